@@ -1,0 +1,150 @@
+/*
+ * paged_attn.h — C ABI of libpaged-attention.so, MI355X (gfx950) build.
+ *
+ * Drop-in for the reference's public header `csrc/paged_attn.h` (installed to
+ * include/ by CMakeLists.txt:78-81): the three reference entry points keep their
+ * exact names, parameter order and types.  Everything else here is new.
+ *
+ * Conventions shared by every entry point (reference semantics):
+ *   - all pointers are caller-owned DEVICE pointers on the current HIP device;
+ *     tensors are contiguous: dense  [batch, seqlen, heads, head_size],
+ *     varlen [total_tokens, heads, head_size], paged [num_blocks, page, heads_k, head_size];
+ *   - head_size must be a multiple of 8 (callers pad, export.cpp:539-547) and <= 256;
+ *   - `is_fp16 == false` means bf16;
+ *   - causality is carried ONLY by the windows: causal <=> window_left < 0 && window_right == 0
+ *     (paged_attn.cpp:116); the `is_causal` flags of the varlen/paged entries are ignored,
+ *     exactly as in the reference;
+ *   - work is enqueued asynchronously on `stream`; nothing synchronises;
+ *   - errors never throw or exit: the call returns without launching and the reason is
+ *     readable from fmha_last_error() on the calling thread (""/NULL-free on success).
+ */
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define FMHA_DEFAULT(x) = x
+extern "C" {
+#else
+#define FMHA_DEFAULT(x)
+#endif
+
+/* Dense forward.  Replaces csrc/paged_attn.h:8-31 (impl paged_attn.cpp:310-383).
+ * Writes o and, when softmax_lse_ptr != NULL, the fp32 log-sum-exp [batch, heads, seqlen_q]
+ * (the reference leaves it unwritten; bwd needs it).  alibi_slopes_ptr: fp32 [heads] or
+ * [batch, heads] (the latter when batch > 1, as paged_attn.cpp:375 assumes).  Dropout and
+ * return_softmax are not supported on the C path (the reference's split kernel ignores them,
+ * SURVEY §8a (ii)): p_dropout > 0 is rejected with an error.  num_splits <= 0 picks a split
+ * count; 1 forces the single-pass kernel. */
+void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_slopes_ptr,
+              const int32_t seqlen_q, const int32_t seqlen_k, const int32_t batch_size,
+              const int32_t num_heads, const int32_t num_heads_k, const int32_t head_size,
+              const float p_dropout, hipStream_t stream, hipDeviceProp_t* dprops,
+              const float softmax_scale, void* p_ptr, void* softmax_lse_ptr,
+              int window_size_left, int window_size_right, const float softcap,
+              const bool return_softmax, bool is_fp16, int num_splits FMHA_DEFAULT(0));
+
+/* Varlen (packed, ragged) forward.  Replaces csrc/paged_attn.h:33-53 (impl
+ * paged_attn.cpp:385-440).  cu_seqlens_{q,k}: int32 [batch+1], cumulative. */
+void fmha_varlen_fwd(void* q_ptrs, void* k_ptrs, void* v_ptrs, void* o_ptrs,
+                     void* cu_seqlens_q_ptrs, void* cu_seqlens_k_ptrs,
+                     const int32_t max_seqlen_q, const int32_t max_seqlen_k,
+                     const int32_t batch_size, const int32_t num_heads,
+                     const int32_t num_heads_k, const int32_t head_size, hipStream_t stream,
+                     const float softmax_scale, const bool is_causal, const bool is_fp16,
+                     int window_size_left FMHA_DEFAULT(-1), int window_size_right FMHA_DEFAULT(-1));
+
+/* Paged-KV forward (decode / chunked prefill over a block table).  Replaces
+ * csrc/paged_attn.h:55-84 (impl paged_attn.cpp:442-568).
+ * kcache/vcache [num_blocks, page_block_size, heads_k, head_size]; block_table int32
+ * [batch, max_cache_seq_k / page_block_size]; cache_seqlens_k int32 [batch] = per-sequence
+ * lengths (non-cumulative).  k/v (append), cache_batch_idx and rotary are ignored exactly
+ * as in the reference C path (paged_attn.cpp:513-525).  Split scratch comes from a cached
+ * per-device pool (no per-call hipMalloc, no leak — cf. paged_attn.cpp:186-189,557-561). */
+void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void* k_ptr,
+                           void* v_ptr, void* o_ptr, void* block_table_ptr,
+                           void* cache_seqlens_k_ptr, const int32_t max_cache_seq_k,
+                           const int32_t seqlen_q, const int32_t seqlen_k,
+                           const int32_t batch_size, const int32_t num_heads,
+                           const int32_t num_heads_k, const int32_t head_size,
+                           const int32_t page_block_size, hipStream_t stream,
+                           const float softmax_scale, int window_size_left,
+                           int window_size_right, const int32_t num_splits,
+                           void* cache_batch_idx_ptr, void* rotary_cos_ptr, void* rotary_sin_ptr,
+                           bool is_causal, bool is_rotary_interleaved, bool is_fp16);
+
+/* ---------------------------------------------------------------- new entry points --- */
+
+/* Thread-local description of the last failed call on this thread ("" if none). */
+const char* fmha_last_error(void);
+/* 0 if the last call on this thread succeeded, a nonzero code otherwise. */
+int fmha_last_status(void);
+
+/* Library version / build identification, e.g. "xf-fmha-gfx950 1.0". */
+const char* fmha_version(void);
+
+/* Varlen forward with the fields the reference's varlen C entry drops (paged_attn.cpp:423-433):
+ * LSE out (fp32 [num_heads, total_q], unpadded as export.cpp:827; total_q = cu_seqlens_q[batch]
+ * must be passed by the caller, it is only used to address the LSE), ALiBi, softcap,
+ * seqused_k (int32 [batch], optional), and an optional paged K/V (block_table != NULL: k/v are
+ * [num_blocks, page, heads_k, head_size], block_table [batch, block_table_stride]). */
+void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
+                        void* cu_seqlens_q, void* cu_seqlens_k, void* seqused_k,
+                        void* block_table, int32_t block_table_stride, int32_t page_block_size,
+                        void* alibi_slopes, int32_t alibi_batch_stride,
+                        int32_t max_seqlen_q, int32_t max_seqlen_k, int32_t total_q,
+                        int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
+                        int32_t head_size, float softmax_scale, int window_size_left,
+                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream);
+
+/* Paged-KV forward that also returns LSE (fp32 [batch, num_heads, seqlen_q]) and takes ALiBi
+ * and an fp8 (OCP e4m3fn) K/V cache with per-tensor dequant scales.
+ * kv_dtype: 0 = same as q (fp16/bf16), 1 = fp8 e4m3fn (k_scale/v_scale multiply the stored
+ * values).  num_splits <= 0 picks a split count. */
+void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
+                              void* block_table, int32_t block_table_stride, void* cache_seqlens,
+                              int32_t seqlen_q, int32_t max_seqlen_k, int32_t batch_size,
+                              int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                              int32_t page_block_size, float softmax_scale,
+                              int window_size_left, int window_size_right, float softcap,
+                              void* alibi_slopes, int32_t alibi_batch_stride, int32_t num_splits,
+                              int32_t kv_dtype, float k_scale, float v_scale, bool is_fp16,
+                              hipStream_t stream);
+
+/* Dense backward: the C form of mha_bwd (export.cpp:948-1176, live twin flash_api_hip.cpp:
+ * 815-1043), which the reference never built.  Inputs dout/q/k/v/out as the fwd layout,
+ * softmax_lse fp32 [batch, heads, seqlen_q] from fmha_fwd; outputs dq [b,sq,h,d],
+ * dk/dv [b,sk,hk,d] (GQA groups reduced in-kernel, no host sum_out), softmax_d fp32
+ * [batch, heads, seqlen_q] (may be NULL: then pool scratch is used).
+ * workspace: optional caller scratch of fmha_bwd_workspace_size() bytes; NULL = pool. */
+void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
+              void* dq, void* dk, void* dv, void* alibi_slopes, void* softmax_d,
+              int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
+              int32_t num_heads_k, int32_t head_size, float p_dropout, float softmax_scale,
+              int window_size_left, int window_size_right, float softcap, bool deterministic,
+              bool is_fp16, hipStream_t stream, void* workspace, size_t workspace_bytes);
+
+size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
+                               int32_t num_heads, int32_t num_heads_k, int32_t head_size);
+
+/* Varlen backward (mha_varlen_bwd semantics, flash_api_hip.cpp:1045-1298): packed q/k/v/out/
+ * dout, cu_seqlens int32 [batch+1], softmax_lse fp32 [num_heads, total_q]. */
+void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
+                     void* dq, void* dk, void* dv, void* cu_seqlens_q, void* cu_seqlens_k,
+                     void* alibi_slopes, int32_t alibi_batch_stride, int32_t max_seqlen_q,
+                     int32_t max_seqlen_k, int32_t total_q, int32_t total_k,
+                     int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
+                     int32_t head_size, float softmax_scale, int window_size_left,
+                     int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
+                     void* workspace, size_t workspace_bytes);
+
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t total_k, int32_t batch_size,
+                                      int32_t num_heads, int32_t num_heads_k, int32_t head_size);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#undef FMHA_DEFAULT

@@ -1,0 +1,244 @@
+"""GPU parity: the gfx950 forward kernels vs the reference oracle.
+
+Pass rule = the reference's own (test.py:975, 1296, 1593-1594): max|out - out_ref| must be at
+most 2x (fwd, varlen) or 3x + 1e-5 (kvcache) the error of the low-precision PyTorch path
+max|out_pt - out_ref|.  LSE (fp32) is checked against oracle.attention_lse_ref with an absolute
+tolerance of 2e-3 (it accumulates in fp32 from the same fp16/bf16 inputs).
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import attention_ref as orc
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LSE_ATOL = 2e-3
+
+
+@pytest.fixture(scope="module")
+def xfa():
+    import xf_flash_attention_cutlass_amd as m
+    return m
+
+
+def _dtype(name):
+    return {"float16": torch.float16, "bfloat16": torch.bfloat16}[name]
+
+
+def _assert_parity(out, out_ref, out_pt, mult=2.0, atol=0.0, what=""):
+    ok, err, bound = orc.parity_ok(out.cpu(), out_ref, out_pt, mult, atol)
+    assert ok, f"{what}: max|out-ref|={err:.3g} > bound {bound:.3g}"
+
+
+@pytest.mark.parametrize("name", [n for n in gu.names("fwd") if "fp32" not in n])
+def test_fwd_golden(xfa, name):
+    t, m = gu.load(name)
+    q, k, v = (t[x].to(DEV) for x in ("q", "k", "v"))
+    slopes = t["alibi_slopes"].to(DEV) if m["alibi"] else None
+    out, lse, _ = xfa.flash_attn_func(q, k, v, 0.0, causal=m["causal"],
+                                      window_size=tuple(m["window"]), softcap=m["softcap"],
+                                      alibi_slopes=slopes, return_attn_probs=True)
+    torch.cuda.synchronize()
+    _assert_parity(out, t["out_ref"], t["out_pt"], what=name)
+    bias = None
+    if m["alibi"]:
+        bias = orc.alibi_bias(t["alibi_slopes"], m["sq"], m["sk"], causal=False)
+    lse_ref = orc.attention_lse_ref(t["q"], t["k"], attn_bias=bias, causal=m["causal"],
+                                    window_size=tuple(m["window"]), softcap=m["softcap"])
+    fin = torch.isfinite(lse_ref)
+    assert torch.equal(torch.isinf(lse.cpu()), ~fin)
+    assert (lse.cpu()[fin] - lse_ref[fin]).abs().max().item() < LSE_ATOL
+
+
+def _rand_case(b, h, hk, sq, sk, d, dtype, causal, window=(-1, -1), seed=0):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(b, sq, h, d, generator=g).to(dtype)
+    k = torch.randn(b, sk, hk, d, generator=g).to(dtype)
+    v = torch.randn(b, sk, hk, d, generator=g).to(dtype)
+    out_ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
+    out_pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False,
+                                  reorder_ops=True)
+    return q, k, v, out_ref, out_pt
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("sq,sk,h,hk", [(1, 147, 4, 4), (113, 203, 4, 2), (128, 217, 2, 1),
+                                        (512, 256, 2, 2), (1023, 1024, 2, 2), (2048, 2048, 1, 1),
+                                        (300, 300, 6, 3)])
+def test_fwd_random(xfa, dtype, causal, d, sq, sk, h, hk):
+    q, k, v, out_ref, out_pt = _rand_case(1, h, hk, sq, sk, d, dtype, causal)
+    out, lse, _ = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal,
+                                      return_attn_probs=True)
+    _assert_parity(out, out_ref, out_pt, what=f"{sq}x{sk} h{h}/{hk} d{d} c{causal}")
+    lse_ref = orc.attention_lse_ref(q, k, causal=causal)
+    fin = torch.isfinite(lse_ref)
+    assert torch.equal(torch.isinf(lse.cpu()), ~fin)
+    assert (lse.cpu()[fin] - lse_ref[fin]).abs().max().item() < LSE_ATOL
+
+
+@pytest.mark.parametrize("window", [(0, 0), (17, 3), (100, -1), (-1, 40), (5, 200)])
+def test_fwd_local_windows(xfa, window):
+    q, k, v, out_ref, out_pt = _rand_case(2, 4, 2, 211, 333, 128, torch.bfloat16, False, window)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), window_size=window)
+    _assert_parity(out, out_ref, out_pt, what=f"window {window}")
+
+
+@pytest.mark.parametrize("d", [40, 80, 96, 104])
+def test_fwd_padded_head_dims(xfa, d):
+    q, k, v, out_ref, out_pt = _rand_case(2, 3, 3, 77, 190, d, torch.float16, True)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=True)
+    assert out.shape == (2, 77, 3, d)
+    _assert_parity(out, out_ref, out_pt, what=f"d={d}")
+
+
+def test_fwd_alibi_softcap_combo(xfa):
+    torch.manual_seed(3)
+    b, h, sq, sk, d = 2, 4, 150, 150, 64
+    q = (torch.randn(b, sq, h, d) * 5).half()
+    k, v = torch.randn(b, sk, h, d).half(), torch.randn(b, sk, h, d).half()
+    slopes = torch.rand(h) * 0.3
+    bias = orc.alibi_bias(slopes.expand(b, h), sq, sk, causal=True)
+    out_ref, _ = orc.attention_ref(q, k, v, attn_bias=bias, causal=True, softcap=30.0)
+    out_pt, _ = orc.attention_ref(q, k, v, attn_bias=bias, causal=True, softcap=30.0,
+                                  upcast=False, reorder_ops=True)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=True, softcap=30.0,
+                              alibi_slopes=slopes.to(DEV))   # [H]-shaped slopes, B > 1
+    _assert_parity(out, out_ref, out_pt, mult=5.0, what="alibi+softcap")
+
+
+def test_fwd_capi_matches_pybind_bitwise(xfa):
+    """The C ABI called directly (ctypes, no torch types) gives the pybind op's bytes."""
+    from xf_flash_attention_cutlass_amd import capi
+    q, k, v, _, _ = _rand_case(2, 8, 2, 257, 300, 128, torch.bfloat16, True)
+    q, k, v = q.to(DEV), k.to(DEV), v.to(DEV)
+    ref = xfa.flash_attn_func(q, k, v, causal=True)
+    o = torch.empty_like(q)
+    lse = torch.empty(2, 8, 257, device=DEV)
+    L = capi.lib()
+    L.fmha_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), None, 257, 300, 2, 8, 2,
+               128, 0.0, capi.stream_handle(), None, 128 ** -0.5, None, lse.data_ptr(), -1, 0,
+               0.0, False, False, 0)
+    capi.check()
+    torch.cuda.synchronize()
+    assert torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("splits", [2, 3, 7])
+def test_fwd_split_kv_matches_single_pass(xfa, splits):
+    from xf_flash_attention_cutlass_amd import capi
+    q, k, v, out_ref, out_pt = _rand_case(1, 4, 4, 64, 1000, 128, torch.float16, False)
+    q, k, v = q.to(DEV), k.to(DEV), v.to(DEV)
+    outs = []
+    for s in (1, splits):
+        o = torch.empty_like(q)
+        lse = torch.empty(1, 4, 64, device=DEV)
+        capi.lib().fmha_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), None, 64,
+                            1000, 1, 4, 4, 128, 0.0, capi.stream_handle(), None, 128 ** -0.5,
+                            None, lse.data_ptr(), -1, -1, 0.0, False, True, s)
+        capi.check()
+        outs.append((o, lse))
+    torch.cuda.synchronize()
+    _assert_parity(outs[1][0], out_ref, out_pt, what=f"splits={splits}")
+    assert (outs[0][1] - outs[1][1]).abs().max().item() < 1e-4
+    assert (outs[0][0].float() - outs[1][0].float()).abs().max().item() < 2e-3
+
+
+def test_fwd_sq_gt_sk_causal_empty_rows(xfa):
+    """Bottom-right causal alignment: with sq > sk the first sq-sk rows see no key -> O = 0,
+    LSE = +inf (flash_fwd_kernel_hip.h:626-670)."""
+    q, k, v, out_ref, out_pt = _rand_case(1, 2, 2, 300, 100, 64, torch.bfloat16, True)
+    out, lse, _ = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=True,
+                                      return_attn_probs=True)
+    assert (out[:, :200].float() == 0).all()
+    assert torch.isinf(lse[:, :, :200]).all()
+    _assert_parity(out, out_ref, out_pt, what="sq>sk causal")
+
+
+def test_fwd_out_param_and_errors(xfa):
+    q = torch.randn(1, 16, 2, 64, device=DEV, dtype=torch.float16)
+    out = torch.empty_like(q)
+    r = xfa.paged_attn.fwd(q, q, q, out, None, 0.0, 0.125, False, -1, -1, 0.0, False, None)
+    assert r[0].data_ptr() == out.data_ptr()
+    with pytest.raises(RuntimeError, match="fp16 and bf16"):
+        xfa.paged_attn.fwd(q.float(), q.float(), q.float(), None, None, 0.0, 0.125, False, -1,
+                           -1, 0.0, False, None)
+    with pytest.raises(RuntimeError, match="must divide"):
+        xfa.flash_attn_func(torch.randn(1, 16, 3, 64, device=DEV, dtype=torch.float16),
+                            q, q)
+
+
+# ----------------------------------------------------------------------------- varlen ----
+@pytest.mark.parametrize("name", gu.names("varlen"))
+def test_varlen_golden(xfa, name):
+    t, m = gu.load(name)
+    qpm, kpm = t["query_padding_mask"], t["key_padding_mask"]
+    q_u, idx_q, cu_q, max_q = orc.unpad_input(t["q"], qpm)
+    k_u, _, cu_k, max_k = orc.unpad_input(t["k"], kpm)
+    v_u, _, _, _ = orc.unpad_input(t["v"], kpm)
+    out_u, lse, _ = xfa.flash_attn_varlen_func(
+        q_u.to(DEV), k_u.to(DEV), v_u.to(DEV), cu_q.to(DEV), cu_k.to(DEV), max_q, max_k,
+        causal=m["causal"], window_size=tuple(m["window"]), return_attn_probs=True)
+    out = orc.pad_input(out_u.cpu(), idx_q, m["b"], m["sq"])
+    _assert_parity(out, t["out_ref"], t["out_pt"], what=name)
+    assert lse.shape == (m["h"], q_u.shape[0])
+
+
+def test_varlen_ragged_large(xfa):
+    """Ragged lengths incl. 1-token and empty-key sequences; compared per sequence."""
+    torch.manual_seed(0)
+    h, hk, d = 4, 2, 128
+    lq = [1, 300, 77, 1024, 5, 640]
+    lk = [147, 300, 500, 1024, 1, 700]
+    cu_q = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(sum(lq), h, d).bfloat16()
+    k = torch.randn(sum(lk), hk, d).bfloat16()
+    v = torch.randn(sum(lk), hk, d).bfloat16()
+    for causal in (False, True):
+        out = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu_q.to(DEV),
+                                         cu_k.to(DEV), max(lq), max(lk), causal=causal).cpu()
+        for i in range(len(lq)):
+            qs = q[cu_q[i]:cu_q[i + 1]][None]
+            ks, vs = k[cu_k[i]:cu_k[i + 1]][None], v[cu_k[i]:cu_k[i + 1]][None]
+            r, _ = orc.attention_ref(qs, ks, vs, causal=causal)
+            pt, _ = orc.attention_ref(qs, ks, vs, causal=causal, upcast=False, reorder_ops=True)
+            _assert_parity(out[cu_q[i]:cu_q[i + 1]][None], r, pt, what=f"seq {i} c{causal}")
+
+
+# ----------------------------------------------------------------------------- kvcache ---
+@pytest.mark.parametrize("name", gu.names("kvcache"))
+def test_kvcache_golden(xfa, name):
+    t, m = gu.load(name)
+    out = xfa.flash_attn_with_kvcache(
+        t["q"].to(DEV), t["k_cache_paged"].to(DEV), t["v_cache_paged"].to(DEV),
+        cache_seqlens=t["cache_seqlens"].to(DEV), block_table=t["block_table"].to(DEV),
+        causal=m["causal"], window_size=tuple(m["window"]), num_splits=m["num_splits"])
+    _assert_parity(out, t["out_ref"], t["out_pt"], mult=3.0, atol=1e-5, what=name)
+
+
+@pytest.mark.parametrize("num_splits", [1, 0, 4])
+@pytest.mark.parametrize("sq,hk", [(1, 8), (4, 2), (64, 4)])
+def test_paged_indexing_bitexact(xfa, num_splits, sq, hk):
+    """Paged O == O over the contiguous gather of the same pages, bit for bit."""
+    torch.manual_seed(0)
+    b, h, d, page, sk = 3, 8, 128, 16, 1000
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    q = torch.randn(b, sq, h, d).bfloat16().to(DEV)
+    seqlens = torch.tensor([1000, 517, 33], dtype=torch.int32).to(DEV)
+    paged = xfa.flash_attn_with_kvcache(q, kp.to(DEV), vp.to(DEV), cache_seqlens=seqlens,
+                                        block_table=table.to(DEV), num_splits=num_splits)
+    nblk = table.shape[1]
+    kfull = kp[table.long().flatten()].reshape(b, nblk * page, hk, d).to(DEV)
+    vfull = vp[table.long().flatten()].reshape(b, nblk * page, hk, d).to(DEV)
+    dense = xfa.flash_attn_with_kvcache(q, kfull, vfull, cache_seqlens=seqlens,
+                                        num_splits=num_splits)
+    assert torch.equal(paged, dense)
+    kpm = torch.arange(sk).view(1, -1) < seqlens.cpu().view(-1, 1)
+    r, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm)
+    pt, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm, upcast=False, reorder_ops=True)
+    _assert_parity(paged, r, pt, mult=3.0, atol=1e-5, what="paged")

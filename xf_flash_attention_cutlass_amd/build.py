@@ -1,0 +1,141 @@
+"""Build the gfx950 native code in-tree (no cmake/ninja needed for the C ABI).
+
+Produces
+  xf_flash_attention_cutlass_amd/lib/libpaged-attention.so   — the C-ABI library
+      (include/paged_attn.h; replaces the reference's CMake target `paged-attention`,
+      CMakeLists.txt:29-33), hipcc --offload-arch=gfx950, no torch dependency;
+  xf_flash_attention_cutlass_amd/lib/paged_attn*.so          — the pybind/ATen module
+      `paged_attn` (export.cpp equivalent), linked against libpaged-attention.so.
+
+Usage: python -m xf_flash_attention_cutlass_amd.build [--no-ext] [-j N] [--force]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+OBJ = os.path.join(PKG, "lib", "obj")
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("XFA_ARCH", "gfx950")
+LIBNAME = "libpaged-attention.so"
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-I", CSRC, "-I", INCLUDE]
+
+VARIANTS = [(hd, dt) for hd in (64, 128) for dt in ("bf16", "f16")]
+
+
+def _newer(out: str, deps) -> bool:
+    if not os.path.exists(out):
+        return False
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+
+
+def _compile(job):
+    src, out, defs = job
+    deps = [src, __file__] + _headers()
+    if _newer(out, deps):
+        return out, None
+    cmd = [HIPCC, *HIP_FLAGS, *defs, "-c", src, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return out, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return out, None
+
+
+def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    todo = []
+    for hd, dt in VARIANTS:
+        defs = [f"-DXFA_HD={hd}", f"-DXFA_DTN={dt}", f"-DXFA_DT_BF16={1 if dt == 'bf16' else 0}"]
+        for kind in ("fwd", "bwd"):
+            src = os.path.join(CSRC, f"fmha_{kind}.hip")
+            todo.append((src, os.path.join(OBJ, f"fmha_{kind}_hd{hd}_{dt}.o"), defs))
+    todo.append((os.path.join(CSRC, "fmha_api.cpp"), os.path.join(OBJ, "fmha_api.o"), []))
+    if force:
+        for _, out, _ in todo:
+            if os.path.exists(out):
+                os.remove(out)
+    errors = []
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for out, err in ex.map(_compile, todo):
+            if err:
+                errors.append(err)
+            elif verbose:
+                print("built", os.path.relpath(out, ROOT))
+    if errors:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
+    objs = [o for _, o, _ in todo]
+    so = os.path.join(LIB, LIBNAME)
+    if not _newer(so, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so, *objs,
+               "-Wl,-soname," + LIBNAME]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return so
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(LIB, "paged_attn" + suffix)
+
+
+def build_ext(force: bool = False, verbose: bool = False) -> str:
+    """pybind11/ATen module `paged_attn` (export.cpp:1757-1764 equivalent), built with g++
+    against torch's headers and linked to libpaged-attention.so (rpath $ORIGIN)."""
+    import torch
+    from torch.utils import cpp_extension as ce
+    src = os.path.join(CSRC, "paged_attn_ext.cpp")
+    out = ext_path()
+    deps = [src, __file__, os.path.join(LIB, LIBNAME)] + _headers()
+    if not force and _newer(out, deps):
+        return out
+    py_inc = sysconfig.get_paths()["include"]
+    import pybind11
+    incs = ce.include_paths() + [py_inc, pybind11.get_include(), "/opt/rocm/include", CSRC, INCLUDE]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-w",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=paged_attn",
+           "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           *[f"-I{i}" for i in incs], src, "-o", out,
+           f"-L{LIB}", "-l:" + LIBNAME, "-Wl,-rpath,$ORIGIN",
+           *[f"-L{p}" for p in ce.library_paths()], "-lc10", "-ltorch", "-ltorch_cpu",
+           "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+           "-L/opt/rocm/lib", "-lamdhip64"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"extension build failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--no-ext", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    so = build_lib(a.jobs, a.force, a.verbose)
+    print("built", so)
+    if not a.no_ext:
+        print("built", build_ext(a.force, a.verbose))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,85 @@
+"""ctypes binding of libpaged-attention.so (the C ABI in include/paged_attn.h).
+
+This is the same binding a maintainer would add on the reference side to call the C ABI
+without torch types (INTEGRATION.md shows it).  Tensors are passed as raw device pointers;
+the current torch stream is passed as the hipStream_t.  No fallback: if the native library
+is missing this module raises at import.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpaged-attention.so")
+
+vp, i32, f32, b_, sz = C.c_void_p, C.c_int32, C.c_float, C.c_bool, C.c_size_t
+
+_SIGS = {
+    "fmha_fwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, f32, vp, vp,
+                 C.c_int, C.c_int, f32, b_, b_, C.c_int],
+    "fmha_varlen_fwd": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, f32, b_, b_,
+                        C.c_int, C.c_int],
+    "fmha_page_kvcache_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32,
+                              i32, vp, f32, C.c_int, C.c_int, i32, vp, vp, vp, b_, b_, b_],
+    "fmha_varlen_fwd_ex": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,
+                           i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp],
+    "fmha_page_kvcache_fwd_ex": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32,
+                                 i32, f32, C.c_int, C.c_int, f32, vp, i32, i32, i32, f32, f32, b_,
+                                 vp],
+    "fmha_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
+                 f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz],
+    "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32],
+    "fmha_varlen_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
+                        i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp, vp, sz],
+    "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32],
+    "fmha_last_error": [],
+    "fmha_last_status": [],
+    "fmha_version": [],
+}
+_RES = {"fmha_last_error": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
+        "fmha_bwd_workspace_size": sz, "fmha_varlen_bwd_workspace_size": sz}
+
+EXPORTED = tuple(_SIGS)
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(f"native library {path} is missing: run `python -m "
+                          "xf_flash_attention_cutlass_amd.build` (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RES.get(name, None)
+    return lib
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = load()
+    return _lib
+
+
+class FmhaError(RuntimeError):
+    pass
+
+
+def check() -> None:
+    """Raise the thread-local error of the last call, if any (mirrors TORCH_CHECK)."""
+    L = lib()
+    if L.fmha_last_status() != 0:
+        raise FmhaError(L.fmha_last_error().decode())
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

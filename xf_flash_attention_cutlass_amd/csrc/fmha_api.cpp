@@ -1,0 +1,360 @@
+// fmha_api.cpp — the C ABI of libpaged-attention.so (declared in include/paged_attn.h).
+//
+// Re-implements the reference's L3 boundary (csrc/paged_attn.cpp:6-568): parameter packing
+// (set_params_fprop_strided :6-126), the split heuristic (:128-163), split scratch (:165-196)
+// and the three entry points (:310-568) — plus fmha_bwd / varlen / _ex entries the reference
+// lacks.  Differences by design:
+//   * no exceptions or exit() cross the ABI: failures set a thread-local error and return;
+//   * split scratch comes from a cached per-(device, stream) pool — no hipMalloc/hipFree per call
+//     (the reference mallocs every call and leaks, paged_attn.cpp:186-189,557-561);
+//   * the current device is used (the reference queries device 0, :527-528);
+//   * LSE is written whenever a pointer is given.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/paged_attn.h"
+#include "fmha_launch.h"
+
+using namespace xfa;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local int g_status = 0;
+
+void clear_error() { g_err.clear(); g_status = 0; }
+bool fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+bool fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    g_status = code;
+    return false;
+}
+#define REQUIRE(cond, ...) do { if (!(cond)) { fail(1, __VA_ARGS__); return; } } while (0)
+
+bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    return fail(2, "%s: %s", what, hipGetErrorString(e));
+}
+
+// ---------------------------------------------------------------- scratch pool ---------
+// One growable device buffer per (device, stream).  Work on a stream is ordered, so reuse
+// by the next call on the same stream is safe; growth frees the old block (hipFree waits).
+struct PoolEntry { void* ptr = nullptr; size_t bytes = 0; };
+std::mutex g_pool_mu;
+std::map<std::pair<int, hipStream_t>, PoolEntry> g_pool;
+
+void* pool_get(hipStream_t st, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    PoolEntry& e = g_pool[{dev, st}];
+    if (e.bytes >= bytes) return e.ptr;
+    if (e.ptr) { hipStreamSynchronize(st); hipFree(e.ptr); e.ptr = nullptr; e.bytes = 0; }
+    size_t want = bytes + (bytes >> 3) + 4096;
+    if (hipMalloc(&e.ptr, want) != hipSuccess) { e.ptr = nullptr; return nullptr; }
+    e.bytes = want;
+    return e.ptr;
+}
+
+int g_num_cus = 0;
+int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0, n = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        g_num_cus = n;
+    }
+    return g_num_cus;
+}
+
+// Reference heuristic (paged_attn.cpp:128-163): the smallest split count whose wave
+// efficiency reaches 85% of the best, capped at 128.  "SMs" = CUs x resident workgroups.
+int num_splits_heuristic(int work_blocks, int slots, int n_blocks, int max_splits) {
+    if (work_blocks >= 0.8f * slots) return 1;
+    max_splits = std::min(std::min(max_splits, slots), n_blocks);
+    if (max_splits <= 1) return 1;
+    auto cdiv = [](int a, int b) { return (a + b - 1) / b; };
+    std::vector<float> eff(max_splits + 1, 0.f);
+    float best = 0.f;
+    for (int s = 1; s <= max_splits; ++s) {
+        if (s > 1 && cdiv(n_blocks, s) == cdiv(n_blocks, s - 1)) continue;
+        float waves = float(work_blocks * s) / slots;
+        eff[s] = waves / std::ceil(waves);
+        best = std::max(best, eff[s]);
+    }
+    for (int s = 1; s <= max_splits; ++s) {
+        if (s > 1 && cdiv(n_blocks, s) == cdiv(n_blocks, s - 1)) continue;
+        if (eff[s] >= 0.85f * best) return s;
+    }
+    return 1;
+}
+
+int hd_bucket(int d) { return d <= 64 ? 64 : (d <= 128 ? 128 : 256); }
+
+hipError_t dispatch_fwd(const FwdParams& p, bool bf16, hipStream_t st) {
+    const int hd = hd_bucket(p.d);
+    if (hd == 64) return bf16 ? launch_fwd_hd64_bf16(p, st) : launch_fwd_hd64_f16(p, st);
+    if (hd == 128) return bf16 ? launch_fwd_hd128_bf16(p, st) : launch_fwd_hd128_f16(p, st);
+    return hipErrorInvalidValue;
+}
+
+hipError_t dispatch_bwd(const BwdParams& p, bool bf16, hipStream_t st) {
+    const int hd = hd_bucket(p.d);
+    if (hd == 64) return bf16 ? launch_bwd_hd64_bf16(p, st) : launch_bwd_hd64_f16(p, st);
+    if (hd == 128) return bf16 ? launch_bwd_hd128_bf16(p, st) : launch_bwd_hd128_f16(p, st);
+    return hipErrorInvalidValue;
+}
+
+// Score scaling as set_params_fprop_strided (paged_attn.cpp:93-102): with softcap the
+// kernel computes tanh(s * scale / cap) and then scales by cap.
+void set_scales(FwdParams& p, float softmax_scale, float softcap) {
+    float scale_softmax;
+    if (softcap > 0.f) { p.softcap_pre = softmax_scale / softcap; scale_softmax = softcap; }
+    else { p.softcap_pre = 0.f; scale_softmax = softmax_scale; }
+    p.scale_log2 = scale_softmax * 1.4426950408889634f;
+    p.alibi_mul = 1.f / scale_softmax;
+}
+
+// Window normalisation (paged_attn.cpp:116-120): causal <=> wl < 0 && wr == 0.
+void set_windows(int& wl, int& wr, int seqlen_k) {
+    if (wl < 0 && wr >= 0) wl = seqlen_k;
+    if (wl >= 0 && wr < 0) wr = seqlen_k;
+}
+
+bool check_common(const void* q, const void* k, const void* v, const void* o, int b, int h,
+                  int hk, int d) {
+    if (!q || !k || !v || !o) return fail(1, "q/k/v/o must be non-null device pointers");
+    if (b <= 0) return fail(1, "batch size must be positive (got %d)", b);
+    if (h <= 0 || hk <= 0 || h % hk != 0)
+        return fail(1, "Number of heads in key/value must divide number of heads in query (h=%d, hk=%d)", h, hk);
+    if (d <= 0 || d % 8 != 0) return fail(1, "head_size must be a positive multiple of 8 (got %d)", d);
+    if (d > 128) return fail(1, "head_size %d not supported by this build (max 128)", d);
+    return true;
+}
+
+void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
+    p.q_row = (int64_t)h * d;  p.q_head = d; p.q_batch = (int64_t)sq * h * d;
+    p.k_row = (int64_t)hk * d; p.k_head = d; p.k_batch = (int64_t)sk * hk * d;
+    p.v_row = (int64_t)hk * d; p.v_head = d; p.v_batch = (int64_t)sk * hk * d;
+    p.o_row = (int64_t)h * d;  p.o_head = d; p.o_batch = (int64_t)sq * h * d;
+    p.lse_batch = (int64_t)h * sq; p.lse_head = sq;
+}
+
+// Split scratch + launch (shared by every forward entry).
+void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
+    const int n_blocks = (p.seqlen_k + kBlockN - 1) / kBlockN;
+    int splits = num_splits_req;
+    if (p.cu_seqlens_q) splits = 1;  // varlen: single pass (the reference forces it too)
+    if (splits <= 0) {
+        const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group);
+        splits = num_splits_heuristic(work, num_cus() * 2, n_blocks, 128);
+    }
+    splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
+    p.num_splits = splits;
+    if (splits > 1) {
+        const int hd = hd_bucket(p.d);
+        const size_t rows = (size_t)p.b * p.h * p.seqlen_q;
+        const size_t bytes = (size_t)splits * rows * (hd + 1) * sizeof(float);
+        char* base = (char*)pool_get(st, bytes);
+        if (!base) { fail(3, "could not allocate %zu bytes of split scratch", bytes); return; }
+        p.oaccum = (float*)base;
+        p.lseaccum = (float*)(base + (size_t)splits * rows * hd * sizeof(float));
+    }
+    hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fmha_last_error(void) { return g_err.c_str(); }
+int fmha_last_status(void) { return g_status; }
+const char* fmha_version(void) { return "xf-fmha-gfx950 1.0"; }
+
+void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_slopes_ptr,
+              const int32_t seqlen_q, const int32_t seqlen_k, const int32_t batch_size,
+              const int32_t num_heads, const int32_t num_heads_k, const int32_t head_size,
+              const float p_dropout, hipStream_t stream, hipDeviceProp_t* /*dprops*/,
+              const float softmax_scale, void* /*p_ptr*/, void* softmax_lse_ptr,
+              int window_size_left, int window_size_right, const float softcap,
+              const bool return_softmax, bool is_fp16, int num_splits) {
+    try {
+        clear_error();
+        if (!check_common(q_ptr, k_ptr, v_ptr, o_ptr, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
+        REQUIRE(p_dropout == 0.f, "dropout is not supported by the forward C path (p_dropout=%g)", p_dropout);
+        REQUIRE(!return_softmax, "return_softmax is only supported with dropout, which this build does not support");
+        FwdParams p{};
+        p.q = q_ptr; p.k = k_ptr; p.v = v_ptr; p.o = o_ptr;
+        p.lse = (float*)softmax_lse_ptr;
+        dense_strides(p, seqlen_q, seqlen_k, num_heads, num_heads_k, head_size);
+        p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
+        p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
+        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.wl = window_size_left; p.wr = window_size_right;
+        set_scales(p, softmax_scale, softcap);
+        p.alibi = (const float*)alibi_slopes_ptr;
+        p.alibi_bstride = batch_size > 1 ? num_heads : 0;   // paged_attn.cpp:375
+        run_fwd(p, !is_fp16, stream, num_splits);
+    } catch (...) {
+        fail(9, "internal error in fmha_fwd");
+    }
+}
+
+void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
+                        void* cu_seqlens_q, void* cu_seqlens_k, void* seqused_k,
+                        void* block_table, int32_t block_table_stride, int32_t page_block_size,
+                        void* alibi_slopes, int32_t alibi_batch_stride,
+                        int32_t max_seqlen_q, int32_t max_seqlen_k, int32_t total_q,
+                        int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
+                        int32_t head_size, float softmax_scale, int window_size_left,
+                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream) {
+    try {
+        clear_error();
+        if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(cu_seqlens_q && (cu_seqlens_k || block_table),
+                "cu_seqlens_q and cu_seqlens_k (or a block table) must be given");
+        REQUIRE(max_seqlen_q > 0 && max_seqlen_k >= 0, "max_seqlen_q must be positive");
+        if (max_seqlen_k == 0) { fail(1, "max_seqlen_k == 0: nothing to attend to"); return; }
+        FwdParams p{};
+        p.q = q; p.k = k; p.v = v; p.o = o; p.lse = (float*)softmax_lse;
+        const int h = num_heads, hk = num_heads_k, d = head_size;
+        p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
+        p.o_row = (int64_t)h * d; p.o_head = d; p.o_batch = 0;
+        p.k_row = (int64_t)hk * d; p.k_head = d; p.k_batch = 0;
+        p.v_row = (int64_t)hk * d; p.v_head = d; p.v_batch = 0;
+        p.cu_seqlens_q = (const int*)cu_seqlens_q;
+        if (block_table) {
+            REQUIRE(page_block_size > 0, "page_block_size must be positive");
+            p.block_table = (const int*)block_table;
+            p.bt_stride = block_table_stride;
+            p.page_size = page_block_size;
+            p.k_batch = (int64_t)page_block_size * hk * d;
+            p.v_batch = (int64_t)page_block_size * hk * d;
+            // key lengths from seqused_k or cu_seqlens_k; pages are per sequence (no k offset)
+            p.cu_seqlens_k = (const int*)cu_seqlens_k;
+            REQUIRE(seqused_k || cu_seqlens_k, "paged varlen needs seqused_k or cu_seqlens_k");
+        } else {
+            p.cu_seqlens_k = (const int*)cu_seqlens_k;
+        }
+        p.seqused_k = (const int*)seqused_k;
+        p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
+        p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
+        set_windows(window_size_left, window_size_right, max_seqlen_k);
+        p.wl = window_size_left; p.wr = window_size_right;
+        set_scales(p, softmax_scale, softcap);
+        p.alibi = (const float*)alibi_slopes; p.alibi_bstride = alibi_batch_stride;
+        // unpadded LSE [num_heads, total_q] (export.cpp:827): index = h*total_q + q_off + pos
+        p.lse_batch = 0;
+        p.lse_head = total_q;
+        REQUIRE(!softmax_lse || total_q > 0, "total_q must be given to address the LSE");
+        run_fwd(p, !is_fp16, stream, 1);
+    } catch (...) {
+        fail(9, "internal error in fmha_varlen_fwd_ex");
+    }
+}
+
+void fmha_varlen_fwd(void* q_ptrs, void* k_ptrs, void* v_ptrs, void* o_ptrs,
+                     void* cu_seqlens_q_ptrs, void* cu_seqlens_k_ptrs,
+                     const int32_t max_seqlen_q, const int32_t max_seqlen_k,
+                     const int32_t batch_size, const int32_t num_heads,
+                     const int32_t num_heads_k, const int32_t head_size, hipStream_t stream,
+                     const float softmax_scale, const bool /*is_causal*/, const bool is_fp16,
+                     int window_size_left, int window_size_right) {
+    fmha_varlen_fwd_ex(q_ptrs, k_ptrs, v_ptrs, o_ptrs, nullptr, cu_seqlens_q_ptrs,
+                       cu_seqlens_k_ptrs, nullptr, nullptr, 0, 0, nullptr, 0, max_seqlen_q,
+                       max_seqlen_k, 0, batch_size, num_heads, num_heads_k, head_size,
+                       softmax_scale, window_size_left, window_size_right, 0.f, is_fp16, stream);
+}
+
+void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
+                              void* block_table, int32_t block_table_stride, void* cache_seqlens,
+                              int32_t seqlen_q, int32_t max_seqlen_k, int32_t batch_size,
+                              int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                              int32_t page_block_size, float softmax_scale,
+                              int window_size_left, int window_size_right, float softcap,
+                              void* alibi_slopes, int32_t alibi_batch_stride, int32_t num_splits,
+                              int32_t kv_dtype, float k_scale, float v_scale, bool is_fp16,
+                              hipStream_t stream) {
+    try {
+        clear_error();
+        if (!check_common(q, kcache, vcache, o, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(block_table, "block_table must be given for the paged KV path");
+        REQUIRE(page_block_size > 0, "page_block_size must be positive");
+        REQUIRE(seqlen_q > 0 && max_seqlen_k > 0, "seqlen_q / seqlen_k must be positive");
+        REQUIRE(kv_dtype == 0, "fp8 KV cache is not supported by this build yet");
+        FwdParams p{};
+        const int h = num_heads, hk = num_heads_k, d = head_size;
+        p.q = q; p.k = kcache; p.v = vcache; p.o = o; p.lse = (float*)softmax_lse;
+        dense_strides(p, seqlen_q, max_seqlen_k, h, hk, d);
+        p.k_batch = (int64_t)page_block_size * hk * d;   // page stride (paged_attn.cpp:506-507)
+        p.v_batch = (int64_t)page_block_size * hk * d;
+        p.block_table = (const int*)block_table;
+        p.bt_stride = block_table_stride;
+        p.page_size = page_block_size;
+        p.seqused_k = (const int*)cache_seqlens;         // non-cumulative (paged_attn.cpp:518-519)
+        p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
+        p.seqlen_q = seqlen_q; p.seqlen_k = max_seqlen_k;
+        set_windows(window_size_left, window_size_right, max_seqlen_k);
+        p.wl = window_size_left; p.wr = window_size_right;
+        set_scales(p, softmax_scale, softcap);
+        p.alibi = (const float*)alibi_slopes; p.alibi_bstride = alibi_batch_stride;
+        p.kv_fp8 = kv_dtype == 1; p.k_scale = k_scale; p.v_scale = v_scale;
+        run_fwd(p, !is_fp16, stream, num_splits);
+    } catch (...) {
+        fail(9, "internal error in fmha_page_kvcache_fwd_ex");
+    }
+}
+
+void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void* /*k_ptr*/,
+                           void* /*v_ptr*/, void* o_ptr, void* block_table_ptr,
+                           void* cache_seqlens_k_ptr, const int32_t max_cache_seq_k,
+                           const int32_t seqlen_q, const int32_t seqlen_k,
+                           const int32_t batch_size, const int32_t num_heads,
+                           const int32_t num_heads_k, const int32_t head_size,
+                           const int32_t page_block_size, hipStream_t stream,
+                           const float softmax_scale, int window_size_left,
+                           int window_size_right, const int32_t num_splits,
+                           void* /*cache_batch_idx_ptr*/, void* /*rotary_cos_ptr*/,
+                           void* /*rotary_sin_ptr*/, bool /*is_causal*/,
+                           bool /*is_rotary_interleaved*/, bool is_fp16) {
+    if (page_block_size <= 0) { clear_error(); fail(1, "page_block_size must be positive"); return; }
+    fmha_page_kvcache_fwd_ex(q_ptr, kcache_ptr, vcache_ptr, o_ptr, nullptr, block_table_ptr,
+                             max_cache_seq_k / page_block_size, cache_seqlens_k_ptr, seqlen_q,
+                             seqlen_k, batch_size, num_heads, num_heads_k, head_size,
+                             page_block_size, softmax_scale, window_size_left, window_size_right,
+                             0.f, nullptr, 0, num_splits, 0, 1.f, 1.f, is_fp16, stream);
+}
+
+
+// Backward entry points: filled in by the bwd milestone.
+size_t fmha_bwd_workspace_size(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t) { return 16; }
+size_t fmha_varlen_bwd_workspace_size(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t) { return 16; }
+void fmha_bwd(void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, void*,
+              int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, float, float, int, int, float,
+              bool, bool, hipStream_t, void*, size_t) {
+    clear_error();
+    fail(4, "fmha_bwd: backward not available in this build");
+}
+void fmha_varlen_bwd(void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, void*,
+                     void*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
+                     int32_t, float, int, int, float, bool, hipStream_t, void*, size_t) {
+    clear_error();
+    fail(4, "fmha_varlen_bwd: backward not available in this build");
+}
+
+}  // extern "C"

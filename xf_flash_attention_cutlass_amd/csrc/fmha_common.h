@@ -1,0 +1,169 @@
+// fmha_common.h — shared device/host definitions for the gfx950 attention kernels.
+//
+// Parameter blocks are our own POD structs (the reference packs `Flash_fwd_params`,
+// csrc/flash_attn/src/flash_hip.h:50-172; we keep only what the MI355X kernels read).
+// All strides are in ELEMENTS, like the reference (paged_attn.cpp:45-60).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xfa {
+
+// ------------------------------------------------------------------ vector types --
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kBlockN = 64;   // keys per K/V tile (one LDS stage)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// ------------------------------------------------------------------ params -------
+struct FwdParams {
+    const void* q;
+    const void* k;
+    const void* v;
+    void* o;
+    float* lse;        // optional; index = b*lse_batch + h*lse_head + (q_offset + pos)
+    float* oaccum;     // split scratch [splits][b][h][seqlen_q][HD] fp32
+    float* lseaccum;   // split scratch [splits][b][h][seqlen_q] fp32
+
+    int64_t q_batch, q_row, q_head;
+    int64_t k_batch, k_row, k_head;   // paged: k_batch is the page stride
+    int64_t v_batch, v_row, v_head;
+    int64_t o_batch, o_row, o_head;
+    int64_t lse_batch, lse_head;
+
+    const int* cu_seqlens_q;   // varlen q (cumulative) or null
+    const int* cu_seqlens_k;   // varlen k (cumulative) or null
+    const int* seqused_k;      // per-batch key length (kvcache cache_seqlens / seqused_k) or null
+    const int* block_table;    // paged K/V or null
+    int bt_stride;
+    int page_size;
+    const float* alibi;        // fp32 slopes or null
+    int alibi_bstride;
+
+    int b, h, hk, group, d;
+    int seqlen_q, seqlen_k;    // max lengths for varlen
+    int wl, wr;                // normalised windows (<0 = unbounded)
+    float scale_log2;          // multiplies the working score
+    float softcap_pre;         // >0: w = tanh(s * softcap_pre)
+    float alibi_mul;           // 1 / scale_softmax (bias in working units)
+    int num_splits;
+    int kv_fp8;                // 1: K/V stored as fp8 e4m3fn
+    float k_scale, v_scale;
+};
+
+struct CombineParams {
+    const float* oaccum;
+    const float* lseaccum;
+    void* o;
+    float* lse;
+    int64_t o_batch, o_row, o_head;
+    int64_t lse_batch, lse_head;
+    int b, h, seqlen_q, d, hd, num_splits;
+};
+
+struct BwdParams {
+    const void* q; const void* k; const void* v; const void* o; const void* dout;
+    const float* lse;
+    void* dq; void* dk; void* dv;
+    float* dq_accum;     // fp32 [b][h][seqlen_q_pad][HD] (varlen: [h][total_q_pad][HD])
+    float* dsum;         // fp32 rowsum(dO*O), layout like lse
+    float* dk_accum;     // fp32 GQA partial accumulators or null
+    float* dv_accum;
+
+    int64_t q_batch, q_row, q_head;
+    int64_t k_batch, k_row, k_head;
+    int64_t v_batch, v_row, v_head;
+    int64_t o_batch, o_row, o_head;
+    int64_t do_batch, do_row, do_head;
+    int64_t dq_batch, dq_row, dq_head;
+    int64_t dk_batch, dk_row, dk_head;
+    int64_t dv_batch, dv_row, dv_head;
+    int64_t lse_batch, lse_head;   // lse / dsum index = b*lse_batch + h*lse_head + q_offset + pos
+    int64_t acc_batch, acc_head, acc_row;  // dq_accum strides (floats)
+
+    const int* cu_seqlens_q;
+    const int* cu_seqlens_k;
+    const float* alibi;
+    int alibi_bstride;
+
+    int b, h, hk, group, d;
+    int seqlen_q, seqlen_k;
+    int wl, wr;
+    float scale;         // softmax scale (natural units)
+    float scale_log2;
+    float softcap_pre;
+    float alibi_mul;
+    int softcap_on;
+};
+
+// ------------------------------------------------------------------ dtype traits --
+template <typename T> struct DT;
+template <> struct DT<__bf16> {
+    typedef bf16x8 v8;
+    static __device__ __forceinline__ f32x16 mfma32(const v8& a, const v8& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct DT<_Float16> {
+    typedef f16x8 v8;
+    static __device__ __forceinline__ f32x16 mfma32(const v8& a, const v8& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// Conflict-free 16-byte-chunk swizzle of a [rows][HD] 16-bit LDS tile (HD*2-byte rows),
+// shared by the row reads (ds_read_b128, 32x32x16 A/B operand) and the transposed reads
+// (ds_read_b64_tr_b16) — see DESIGN.md §LDS for the bank derivation.
+template <int HD> __device__ __forceinline__ int swz(int row);
+template <> __device__ __forceinline__ int swz<128>(int row) {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+template <> __device__ __forceinline__ int swz<64>(int row) {
+    return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+template <int HD> __device__ __forceinline__ int lds_off(int row, int chunk) {
+    return row * (HD * 2) + ((chunk ^ swz<HD>(row)) << 4);
+}
+
+__device__ __forceinline__ float wave_max_halves(float x) {
+    // lanes l and l^32 hold the same query row: exchange halves with v_permlane32_swap
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float wave_sum_halves(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// tanh without a libcall (a call would spill every live accumulator):
+// tanh(x) = 1 - 2 / (exp(2x) + 1); saturates correctly at +-inf.
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * (2.f * 1.4426950408889634f));
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+// fp8 e4m3fn (OCP) -> f32, exact.
+__device__ __forceinline__ float fp8e4m3_to_f32(uint32_t b) {
+    uint32_t s = (b & 0x80u) << 24;
+    uint32_t e = (b >> 3) & 0xFu;
+    uint32_t m = b & 0x7u;
+    if (e == 0) {
+        float f = (float)m * 0.001953125f;  // m * 2^-9
+        return s ? -f : f;
+    }
+    if (e == 0xF && m == 0x7) return __uint_as_float(0x7FC00000u);
+    return __uint_as_float(s | ((e + 120u) << 23) | (m << 20));
+}
+
+}  // namespace xfa

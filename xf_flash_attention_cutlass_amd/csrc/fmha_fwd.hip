@@ -1,0 +1,69 @@
+// fmha_fwd.hip — forward instantiations for one (head dim, dtype) pair.
+// Compiled once per pair with -DXFA_HD=<64|128> -DXFA_DT=<bf16|f16> (see build.py), which
+// keeps the per-variant kernels in separate code objects (co-compiled template variants
+// perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
+#include "fmha_fwd_kernel.h"
+#include "fmha_launch.h"
+
+#ifndef XFA_HD
+#error "XFA_HD must be defined"
+#endif
+
+#define XFA_CAT2(a, b) a##b
+#define XFA_CAT(a, b) XFA_CAT2(a, b)
+#define XFA_FN(hd, dt) XFA_CAT(XFA_CAT(XFA_CAT(launch_fwd_hd, hd), _), dt)
+
+namespace xfa {
+
+#if XFA_DT_BF16
+typedef __bf16 elem_t;
+#else
+typedef _Float16 elem_t;
+#endif
+
+template <int HD, typename T>
+static hipError_t launch_fwd_impl(const FwdParams& p, hipStream_t st) {
+    constexpr int NW = kFwdWaves;
+    const bool mask = p.wl >= 0 || p.wr >= 0;
+    const bool feat = p.alibi || p.softcap_pre > 0.f || p.cu_seqlens_q || p.cu_seqlens_k ||
+                      p.seqused_k || p.block_table || p.num_splits > 1 || p.kv_fp8;
+    const dim3 grid(p.b * p.hk, fwd_num_m_blocks(p.seqlen_q, p.group), p.num_splits > 1 ? p.num_splits : 1);
+    const size_t smem = 2 * 2 * kBlockN * HD * 2;
+    void (*kern)(const FwdParams) =
+        mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
+             : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
+    static bool attr_done = false;   // benign race: idempotent attribute set
+    if (!attr_done) {
+        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        attr_done = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.num_splits <= 1) return e;
+
+    CombineParams cp;
+    cp.oaccum = p.oaccum;
+    cp.lseaccum = p.lseaccum;
+    cp.o = p.o;
+    cp.lse = p.lse;
+    cp.o_batch = p.o_batch; cp.o_row = p.o_row; cp.o_head = p.o_head;
+    cp.lse_batch = p.lse_batch; cp.lse_head = p.lse_head;
+    cp.b = p.b; cp.h = p.h; cp.seqlen_q = p.seqlen_q; cp.d = p.d; cp.hd = HD;
+    cp.num_splits = p.num_splits;
+    const int64_t rows = (int64_t)p.b * p.h * p.seqlen_q;
+    hipLaunchKernelGGL((fmha_combine_kernel<HD, T>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, cp);
+    return hipGetLastError();
+}
+
+hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
+    return launch_fwd_impl<XFA_HD, elem_t>(p, st);
+}
+
+}  // namespace xfa

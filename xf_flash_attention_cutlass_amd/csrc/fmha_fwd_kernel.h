@@ -1,0 +1,365 @@
+// fmha_fwd_kernel.h — fused QK^T -> online softmax -> PV forward for gfx950 (CDNA4).
+//
+// Replaces the reference's hot kernel `compute_attn_1rowblock_splitkv`
+// (csrc/flash_attn/src/flash_fwd_kernel_hip.h:585-1283) and its combine
+// `combine_attn_seqk_parallel` (:1322-1568).  Same math (online softmax with exp2 and the
+// scale folded into one FMA, bottom-right aligned causal/local windows, ALiBi, softcap,
+// varlen, paged K/V, split-KV + LSE combine), re-designed for CDNA4:
+//
+//  * one workgroup = NW waves; each wave owns 32 query rows -> BLOCK_M = 32*NW rows;
+//    GQA groups are packed into the row dimension (row = pos*G + g), so the G query heads
+//    sharing a K/V head share every K/V tile (the reference swaps only for Sq == 1,
+//    export.cpp:526-532);
+//  * S^T = K * Q^T with v_mfma_f32_32x32x16_{bf16,f16}: the accumulator holds 16 keys of ONE
+//    query row per lane (row = lane & 31), so row max / row sum are lane-local plus one
+//    v_permlane32_swap; the P accumulator is then, after a pairwise cvt, directly the B operand
+//    of O^T += V^T * P^T (no LDS round trip for P) and the O^T accumulator keeps one query row
+//    per lane, so the online-softmax rescale is lane-local too;
+//  * K and V tiles (64 keys x HD) are register-staged into a double-buffered, XOR-swizzled LDS
+//    image (one barrier per tile); K is read with ds_read_b128, V with the gfx950 transposing
+//    ds_read_b64_tr_b16 — both conflict-free on the same image;
+//  * masking runs only on the tiles that cross a window edge; tiles a wave cannot see are
+//    skipped by that wave (wave-uniform branch); the heaviest causal row blocks launch first.
+#pragma once
+
+#include "fmha_common.h"
+
+namespace xfa {
+
+template <int HD, typename T, int NW, bool MASK, bool FEAT>
+__global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p) {
+    using V8 = typename DT<T>::v8;
+    constexpr int NT = NW * 64;
+    constexpr int BM = NW * 32;
+    constexpr int CPR = HD / 8;                 // 16-byte chunks per K/V row
+    constexpr int NLD = kBlockN * CPR / NT;     // chunks per thread per tile
+    constexpr int TILE = kBlockN * HD * 2;      // bytes of one K (or V) tile
+    constexpr int NS = HD / 16;                 // k-steps of the QK^T product
+    constexpr int ND = HD / 32;                 // 32-wide d tiles of O^T
+    static_assert(NLD >= 1 && (NT % CPR) == 0, "tile/thread geometry");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int lr = lane & 31;
+    const int hh = lane >> 5;
+
+    const int bh = blockIdx.x;
+    const int bidx = bh / p.hk;
+    const int hk_i = bh - bidx * p.hk;
+    const int m_block = gridDim.y - 1 - blockIdx.y;   // heaviest (causal) row blocks first
+    const int split = blockIdx.z;
+
+    int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
+    if (FEAT) {
+        if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
+        if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
+        if (p.seqused_k) sk = p.seqused_k[bidx];
+    }
+    const int G = p.group;
+    const int rows_total = sq * G;
+    const int row0 = m_block * BM;
+    if (row0 >= rows_total) return;
+
+    const int diag = sk - sq;
+    // Window limits for query position `pos`: keys [lim_l, lim_r).
+    auto lim_r = [&](int pos) { return (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk; };
+    auto lim_l = [&](int pos) { return (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0; };
+
+    // Key-tile range of the whole workgroup (and of this split).
+    const int pos_lo = row0 / G;
+    const int pos_hi = (min(row0 + BM, rows_total) - 1) / G;
+    const int n_lo = lim_l(pos_lo);
+    const int n_hi = lim_r(pos_hi);
+    int nb_lo = n_lo / kBlockN;
+    int nb_hi = n_hi > n_lo ? (n_hi + kBlockN - 1) / kBlockN : nb_lo;
+    const bool is_split = FEAT && p.num_splits > 1;
+    if (is_split) {
+        const int per = (nb_hi - nb_lo + p.num_splits - 1) / p.num_splits;
+        const int s_lo = nb_lo + split * per;
+        nb_hi = min(nb_hi, s_lo + per);
+        nb_lo = min(s_lo, nb_hi);
+    }
+
+    // This lane's query row.
+    const int wrow0 = row0 + wave * 32;
+    const int row = wrow0 + lr;
+    const bool row_ok = row < rows_total;
+    const int pos = row_ok ? row / G : 0;
+    const int head = hk_i * G + (row_ok ? row - pos * G : 0);
+    const bool wave_ok = wrow0 < rows_total;
+    const int wp_lo = wrow0 / G;
+    const int wp_hi = (min(wrow0 + 32, rows_total) - 1) / G;
+    const int w_lr_min = lim_r(wp_lo), w_lr_max = lim_r(wp_hi);
+    const int w_ll_min = lim_l(wp_lo), w_ll_max = lim_l(wp_hi);
+    const int my_lr = lim_r(pos), my_ll = lim_l(pos);
+
+    float alibi_w = 0.f;
+    if (FEAT && p.alibi) alibi_w = p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul;
+    const float c = p.scale_log2;
+
+    // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][16s + 8hh .. +7]
+    V8 qf[NS];
+    {
+        const T* qrow = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
+                        (int64_t)(q_off + pos) * p.q_row + (int64_t)head * p.q_head;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int d0 = 16 * s + 8 * hh;
+            if (row_ok && d0 < p.d) qf[s] = *reinterpret_cast<const V8*>(qrow + d0);
+            else qf[s] = V8{};
+        }
+    }
+
+    // ---- K/V tile loader (register staged: issue early, write to LDS late)
+    const int lc = tid % CPR;
+    const int lrow0 = tid / CPR;
+    constexpr int LROW_STEP = NT / CPR;
+    const bool lc_ok = lc * 8 < p.d;
+    const T* kbase = reinterpret_cast<const T*>(p.k) + (int64_t)hk_i * p.k_head + lc * 8;
+    const T* vbase = reinterpret_cast<const T*>(p.v) + (int64_t)hk_i * p.v_head + lc * 8;
+    const bool paged = FEAT && p.block_table != nullptr;
+    if (!paged) {
+        kbase += (int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row;
+        vbase += (int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row;
+    }
+    const int* btab = paged ? p.block_table + (int64_t)bidx * p.bt_stride : nullptr;
+
+    uint4 kr[NLD], vr[NLD];
+    auto load_tile = [&](int nb) {
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int n = nb * kBlockN + lrow0 + i * LROW_STEP;
+            const bool ok = lc_ok && n < sk;
+            int64_t ko, vo;
+            if (paged) {
+                const int pg = ok ? btab[n / p.page_size] : 0;
+                const int pr = n - (n / p.page_size) * p.page_size;
+                ko = (int64_t)pg * p.k_batch + (int64_t)pr * p.k_row;
+                vo = (int64_t)pg * p.v_batch + (int64_t)pr * p.v_row;
+            } else {
+                ko = (int64_t)n * p.k_row;
+                vo = (int64_t)n * p.v_row;
+            }
+            kr[i] = ok ? *reinterpret_cast<const uint4*>(kbase + ko) : make_uint4(0, 0, 0, 0);
+            vr[i] = ok ? *reinterpret_cast<const uint4*>(vbase + vo) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* ks = smem + buf * 2 * TILE;
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int r = lrow0 + i * LROW_STEP;
+            *reinterpret_cast<uint4*>(ks + lds_off<HD>(r, lc)) = kr[i];
+            *reinterpret_cast<uint4*>(ks + TILE + lds_off<HD>(r, lc)) = vr[i];
+        }
+    };
+
+    // Per-lane LDS read offsets (row-independent parts of the swizzle).
+    int koff[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) koff[s] = lds_off<HD>(lr, 2 * s + hh);
+    const int q4 = (lane & 15) >> 2;
+    int voff[2][ND];
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+            const int r = 4 * hh + q4 + 8 * part;
+            const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+        }
+    }
+
+    f32x16 acc_o[ND];
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) acc_o[dt] = f32x16{};
+    float m_run = -INFINITY;
+    float l_run = 0.f;
+
+    if (nb_lo < nb_hi) {
+        load_tile(nb_lo);
+        store_tile(0);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int nb = nb_lo; nb < nb_hi; ++nb) {
+        const bool more = nb + 1 < nb_hi;
+        if (more) load_tile(nb + 1);
+        const char* ks = smem + buf * 2 * TILE;
+        const char* vs = ks + TILE;
+        const int n0 = nb * kBlockN;
+        const bool active = wave_ok && n0 < w_lr_max && n0 + kBlockN > w_ll_min;
+        if (active) {
+            // ---- S^T = K Q^T : two 32-key tiles
+            f32x16 st[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const V8 a0 = *reinterpret_cast<const V8*>(ks + koff[s]);
+                const V8 a1 = *reinterpret_cast<const V8*>(ks + 32 * HD * 2 + koff[s]);
+                st[0] = DT<T>::mfma32(a0, qf[s], st[0]);
+                st[1] = DT<T>::mfma32(a1, qf[s], st[1]);
+            }
+            // ---- score transforms + masking (only where a window edge crosses the tile)
+            if (FEAT && p.softcap_pre > 0.f) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) st[kt][r] = fast_tanh(st[kt][r] * p.softcap_pre);
+            }
+            const int keyb = n0 + 4 * hh;
+            if (FEAT && p.alibi) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = keyb + 32 * kt + (r & 3) + 8 * (r >> 2);
+                        st[kt][r] -= alibi_w * (float)abs(pos + diag - key);
+                    }
+            }
+            const bool need_mask = (n0 + kBlockN > w_lr_min) || (n0 < w_ll_max);
+            if (need_mask) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int key = keyb + 32 * kt + (r & 3) + 8 * (r >> 2);
+                        if (key >= my_lr || key < my_ll) st[kt][r] = -INFINITY;
+                    }
+            }
+            // ---- online softmax (lane-local row + one half swap)
+            float mx = st[0][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
+            mx = wave_max_halves(mx);
+            const float m_new = fmaxf(m_run, mx);
+            const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
+            const float alpha = fast_exp2(m_run * c - mref);
+            m_run = m_new;
+            float rs = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float e = fast_exp2(fmaf(st[kt][r], c, -mref));
+                    st[kt][r] = e;
+                    rs += e;
+                }
+            l_run = fmaf(l_run, alpha, rs);
+#pragma unroll
+            for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+            // ---- O^T += V^T P^T : P accumulator registers are the B operand as they stand
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    V8 pb;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) pb[j] = (T)st[kt][8 * sp + j];
+                    const int rbase = (32 * kt + 16 * sp) * HD * 2;
+#pragma unroll
+                    for (int dt = 0; dt < ND; ++dt) {
+                        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s16x4*)(vs + rbase + voff[0][dt]));
+                        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s16x4*)(vs + rbase + voff[1][dt]));
+                        const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+                        acc_o[dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb, acc_o[dt]);
+                    }
+                }
+            }
+        }
+        if (more) store_tile(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // ---- epilogue: normalise, write O (or the split partial) and LSE
+    const float l_full = wave_sum_halves(l_run);
+    const bool empty = (l_full == 0.f) || (l_full != l_full);
+    const float inv = empty ? 1.f : 1.f / l_full;
+    if (!row_ok) return;
+    if (is_split) {
+        const int64_t rid = (((int64_t)split * p.b + bidx) * p.h + head) * p.seqlen_q + pos;
+        float* oa = p.oaccum + rid * HD;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = 32 * dt + 8 * g + 4 * hh;
+                f32x4 v = {acc_o[dt][4 * g] * inv, acc_o[dt][4 * g + 1] * inv,
+                           acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv};
+                *reinterpret_cast<f32x4*>(oa + d) = v;
+            }
+        if (hh == 0) p.lseaccum[rid] = empty ? -INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+        return;
+    }
+    T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
+              (int64_t)(q_off + pos) * p.o_row + (int64_t)head * p.o_head;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int d = 32 * dt + 8 * g + 4 * hh;
+            if (d < p.d) {
+                typedef __attribute__((ext_vector_type(4))) T T4;
+                T4 v = {(T)(acc_o[dt][4 * g] * inv), (T)(acc_o[dt][4 * g + 1] * inv),
+                        (T)(acc_o[dt][4 * g + 2] * inv), (T)(acc_o[dt][4 * g + 3] * inv)};
+                *reinterpret_cast<T4*>(orow + d) = v;
+            }
+        }
+    if (p.lse && hh == 0) {
+        p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] =
+            empty ? INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+    }
+}
+
+// Split-KV combine: lse = log sum_s exp(lse_s); O = sum_s exp(lse_s - lse) O_s
+// (reference combine_attn_seqk_parallel, flash_fwd_kernel_hip.h:1322-1568; empty -> +inf).
+// One wave per (b, h, pos) row.
+template <int HD, typename T>
+__global__ void __launch_bounds__(256) fmha_combine_kernel(const CombineParams cp) {
+    const int lane = threadIdx.x & 63;
+    const int64_t rid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t rows = (int64_t)cp.b * cp.h * cp.seqlen_q;
+    if (rid >= rows) return;
+    const int pos = (int)(rid % cp.seqlen_q);
+    const int head = (int)((rid / cp.seqlen_q) % cp.h);
+    const int bidx = (int)(rid / ((int64_t)cp.seqlen_q * cp.h));
+    float mx = -INFINITY;
+    for (int s = 0; s < cp.num_splits; ++s) mx = fmaxf(mx, cp.lseaccum[s * rows + rid]);
+    float sum = 0.f;
+    if (mx != -INFINITY)
+        for (int s = 0; s < cp.num_splits; ++s) sum += __expf(cp.lseaccum[s * rows + rid] - mx);
+    const bool empty = (mx == -INFINITY) || sum == 0.f;
+    const float lse = empty ? INFINITY : __logf(sum) + mx;
+    constexpr int PER = HD / 64;
+    float acc[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) acc[i] = 0.f;
+    if (!empty) {
+        for (int s = 0; s < cp.num_splits; ++s) {
+            const float w = __expf(cp.lseaccum[s * rows + rid] - lse);
+            const float* oa = cp.oaccum + (s * rows + rid) * HD + lane * PER;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) acc[i] = fmaf(w, oa[i], acc[i]);
+        }
+    }
+    T* orow = reinterpret_cast<T*>(cp.o) + (int64_t)bidx * cp.o_batch + (int64_t)pos * cp.o_row +
+              (int64_t)head * cp.o_head;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int d = lane * PER + i;
+        if (d < cp.d) orow[d] = (T)acc[i];
+    }
+    if (cp.lse && lane == 0)
+        cp.lse[(int64_t)bidx * cp.lse_batch + (int64_t)head * cp.lse_head + pos] = lse;
+}
+
+}  // namespace xfa

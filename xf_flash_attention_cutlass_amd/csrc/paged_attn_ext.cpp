@@ -1,0 +1,486 @@
+// paged_attn_ext.cpp — the PyTorch op surface: pybind11 module `paged_attn`.
+//
+// Mirrors the reference's export.cpp (module export.cpp:1757-1764): `fwd` (mha_fwd,
+// export.cpp:465-667), `varlen_fwd` (mha_varlen_fwd, :669-937), `fwd_kvcache`
+// (mha_fwd_kvcache, :1433-1754) with the same argument lists and return tuples, plus `bwd`
+// and `varlen_bwd`, which the reference has only as dead code (:939-1431).  Every op
+// validates with TORCH_CHECK, allocates outputs, and calls the C ABI of
+// libpaged-attention.so (include/paged_attn.h); errors reported by the C ABI are re-raised
+// as RuntimeError.  Behaviour the reference gets wrong is fixed, not copied:
+// LSE is always written; GQA decode is handled by the kernel's head packing instead of the
+// transposed-view swap (:526-532); a [H]-shaped ALiBi vector is expanded rather than read
+// out of bounds; dropout is rejected instead of silently ignored.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include <limits>
+
+#include "paged_attn.h"
+
+#define CHECK_DEVICE(x) TORCH_CHECK(x.is_cuda(), #x " must be on CUDA")
+#define CHECK_SHAPE(x, ...) \
+    TORCH_CHECK(x.sizes() == torch::IntArrayRef({__VA_ARGS__}), #x " must have shape (" #__VA_ARGS__ ")")
+#define CHECK_CONTIGUOUS(x) TORCH_CHECK(x.is_contiguous(), #x " must be contiguous")
+
+namespace {
+
+void raise_if_failed(const char* op) {
+    if (fmha_last_status() != 0) TORCH_CHECK(false, op, ": ", fmha_last_error());
+}
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+int round8(int x) { return (x + 7) / 8 * 8; }
+
+at::Tensor pad_last(const at::Tensor& t, int d_og) {
+    if (d_og % 8 == 0) return t;
+    return torch::nn::functional::pad(t, torch::nn::functional::PadFuncOptions({0, 8 - d_og % 8}));
+}
+
+void check_qkv_dtype(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+    auto dt = q.dtype();
+    TORCH_CHECK(dt == torch::kFloat16 || dt == torch::kBFloat16,
+                "FlashAttention only support fp16 and bf16 data type");
+    TORCH_CHECK(k.dtype() == dt, "query and key must have the same dtype");
+    TORCH_CHECK(v.dtype() == dt, "query and value must have the same dtype");
+    CHECK_DEVICE(q); CHECK_DEVICE(k); CHECK_DEVICE(v);
+    TORCH_CHECK(q.stride(-1) == 1, "Input tensor must have contiguous last dimension");
+    TORCH_CHECK(k.stride(-1) == 1, "Input tensor must have contiguous last dimension");
+    TORCH_CHECK(v.stride(-1) == 1, "Input tensor must have contiguous last dimension");
+}
+
+// ALiBi slopes as the C ABI wants them: fp32, [b, h] when batch > 1 (paged_attn.cpp:375).
+at::Tensor alibi_for_c(c10::optional<at::Tensor>& a, int b, int h, int64_t* bstride) {
+    if (!a.has_value()) { *bstride = 0; return at::Tensor(); }
+    auto s = a.value();
+    TORCH_CHECK(s.dtype() == torch::kFloat32, "ALiBi slopes must have dtype fp32");
+    CHECK_DEVICE(s);
+    TORCH_CHECK(s.stride(-1) == 1, "ALiBi slopes tensor must have contiguous last dimension");
+    TORCH_CHECK(s.sizes() == torch::IntArrayRef({h}) || s.sizes() == torch::IntArrayRef({b, h}),
+                "ALiBi slopes must have shape (num_heads) or (batch_size, num_heads)");
+    if (s.dim() == 1) s = s.unsqueeze(0).expand({b, h});
+    s = s.contiguous();
+    *bstride = b > 1 ? h : 0;
+    return s;
+}
+
+}  // namespace
+
+std::vector<at::Tensor>
+mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<at::Tensor>& out_,
+        c10::optional<at::Tensor>& alibi_slopes_, const float p_dropout, const float softmax_scale,
+        bool is_causal, int window_size_left, int window_size_right, const float softcap,
+        const bool return_softmax, c10::optional<at::Generator> /*gen_*/) {
+    check_qkv_dtype(q, k, v);
+    const auto sizes = q.sizes();
+    TORCH_CHECK(q.dim() == 4, "q must be (batch, seqlen, heads, head_size)");
+    const int batch_size = sizes[0];
+    const int seqlen_q = sizes[1];
+    const int num_heads = sizes[2];
+    const int head_size_og = sizes[3];
+    const int seqlen_k = k.size(1);
+    const int num_heads_k = k.size(2);
+    TORCH_CHECK(batch_size > 0, "batch size must be postive");
+    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
+    if (window_size_left >= seqlen_k) window_size_left = -1;
+    if (window_size_right >= seqlen_k) window_size_right = -1;
+    if (seqlen_q == 1 && !alibi_slopes_.has_value()) is_causal = false;
+    if (is_causal) window_size_right = 0;
+    CHECK_SHAPE(q, batch_size, seqlen_q, num_heads, head_size_og);
+    CHECK_SHAPE(k, batch_size, seqlen_k, num_heads_k, head_size_og);
+    CHECK_SHAPE(v, batch_size, seqlen_k, num_heads_k, head_size_og);
+
+    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
+    at::Tensor k_padded = pad_last(k, head_size_og).contiguous();
+    at::Tensor v_padded = pad_last(v, head_size_og).contiguous();
+    at::Tensor out;
+    if (out_.has_value()) {
+        out = out_.value();
+        TORCH_CHECK(out.dtype() == q.dtype(), "Output must have the same dtype as inputs");
+        CHECK_DEVICE(out);
+        TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
+        CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size_og);
+        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+    } else {
+        out = torch::empty_like(q_padded);
+    }
+    const int head_size = round8(head_size_og);
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto opts = q.options();
+    auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
+    at::Tensor p;
+    auto rng_state = torch::empty({2}, opts.dtype(torch::kInt64));
+    int64_t alibi_bs = 0;
+    at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
+
+    if (seqlen_k > 0) {
+        fmha_fwd(q_padded.data_ptr(), k_padded.data_ptr(), v_padded.data_ptr(), out.data_ptr(),
+                 alibi.defined() ? alibi.data_ptr() : nullptr, seqlen_q, seqlen_k, batch_size,
+                 num_heads, num_heads_k, head_size, p_dropout, cur_stream(), nullptr, softmax_scale,
+                 nullptr, softmax_lse.data_ptr(), window_size_left, window_size_right, softcap,
+                 return_softmax, q.dtype() == torch::kFloat16, 0);
+        raise_if_failed("fwd");
+    } else {
+        out.zero_();
+        softmax_lse.fill_(std::numeric_limits<float>::infinity());
+    }
+    at::Tensor out_padded = out;
+    if (head_size_og % 8 != 0) out = out.index({"...", torch::indexing::Slice(torch::indexing::None, head_size_og)});
+    if (out_.has_value() && !out_.value().is_same(out)) out_.value().copy_(out), out = out_.value();
+    return {out, q_padded, k_padded, v_padded, out_padded, softmax_lse, p, rng_state};
+}
+
+std::vector<at::Tensor>
+mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+               c10::optional<at::Tensor>& out_, const at::Tensor& cu_seqlens_q,
+               const at::Tensor& cu_seqlens_k, c10::optional<at::Tensor>& seqused_k,
+               c10::optional<at::Tensor>& block_table_, c10::optional<at::Tensor>& alibi_slopes_,
+               int max_seqlen_q, const int max_seqlen_k, const float p_dropout,
+               const float softmax_scale, const bool zero_tensors, bool is_causal,
+               int window_size_left, int window_size_right, const float softcap,
+               const bool return_softmax, c10::optional<at::Generator> /*gen_*/) {
+    check_qkv_dtype(q, k, v);
+    TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
+    TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
+    CHECK_DEVICE(cu_seqlens_q); CHECK_DEVICE(cu_seqlens_k);
+    CHECK_CONTIGUOUS(cu_seqlens_q); CHECK_CONTIGUOUS(cu_seqlens_k);
+    at::Tensor block_table;
+    const bool paged_KV = block_table_.has_value();
+    if (paged_KV) {
+        block_table = block_table_.value();
+        CHECK_DEVICE(block_table);
+        TORCH_CHECK(block_table.dtype() == torch::kInt32, "block_table must have dtype torch.int32");
+        TORCH_CHECK(block_table.stride(-1) == 1, "block_table must have contiguous last dimension");
+    }
+    const auto sizes = q.sizes();
+    const int batch_size = cu_seqlens_q.numel() - 1;
+    const int num_heads = sizes[1];
+    const int head_size_og = sizes[2];
+    const int num_heads_k = paged_KV ? k.size(2) : k.size(1);
+    const int total_q = sizes[0];
+    TORCH_CHECK(batch_size > 0, "batch size must be positive");
+    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
+    const int max_num_blocks_per_seq = !paged_KV ? 0 : block_table.size(1);
+    const int num_blocks = !paged_KV ? 0 : k.size(0);
+    const int page_block_size = !paged_KV ? 1 : k.size(1);
+    if (max_seqlen_q == 1 && !alibi_slopes_.has_value()) is_causal = false;
+    if (is_causal) window_size_right = 0;
+    if (window_size_left >= max_seqlen_k) window_size_left = -1;
+    if (window_size_right >= max_seqlen_k) window_size_right = -1;
+    CHECK_SHAPE(q, total_q, num_heads, head_size_og);
+    if (!paged_KV) {
+        const int total_k = k.size(0);
+        CHECK_SHAPE(k, total_k, num_heads_k, head_size_og);
+        CHECK_SHAPE(v, total_k, num_heads_k, head_size_og);
+    } else {
+        CHECK_SHAPE(k, num_blocks, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(v, num_blocks, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(block_table, batch_size, max_num_blocks_per_seq);
+    }
+    CHECK_SHAPE(cu_seqlens_q, batch_size + 1);
+    CHECK_SHAPE(cu_seqlens_k, batch_size + 1);
+    at::Tensor seqused;
+    if (seqused_k.has_value()) {
+        seqused = seqused_k.value();
+        TORCH_CHECK(seqused.dtype() == torch::kInt32, "seqused_k must have dtype int32");
+        TORCH_CHECK(seqused.is_cuda(), "seqused_k must be on CUDA device");
+        TORCH_CHECK(seqused.is_contiguous(), "seqused_k must be contiguous");
+        CHECK_SHAPE(seqused, batch_size);
+    }
+    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
+    at::Tensor k_padded = pad_last(k, head_size_og).contiguous();
+    at::Tensor v_padded = pad_last(v, head_size_og).contiguous();
+    at::Tensor out;
+    if (out_.has_value()) {
+        out = out_.value();
+        TORCH_CHECK(out.dtype() == q.dtype(), "Output must have the same dtype as inputs");
+        CHECK_DEVICE(out);
+        TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
+        CHECK_SHAPE(out, sizes[0], sizes[1], head_size_og);
+        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+    } else {
+        out = torch::empty_like(q_padded);
+    }
+    const int head_size = round8(head_size_og);
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto opts = q.options();
+    auto softmax_lse = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
+    at::Tensor p;
+    auto rng_state = torch::empty({2}, opts.dtype(torch::kInt64));
+    if (zero_tensors) {
+        out.zero_();
+        softmax_lse.fill_(-std::numeric_limits<float>::infinity());
+    }
+    int64_t alibi_bs = 0;
+    at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
+    if (max_seqlen_k > 0) {
+        fmha_varlen_fwd_ex(q_padded.data_ptr(), k_padded.data_ptr(), v_padded.data_ptr(),
+                           out.data_ptr(), softmax_lse.data_ptr(), cu_seqlens_q.data_ptr(),
+                           cu_seqlens_k.data_ptr(), seqused.defined() ? seqused.data_ptr() : nullptr,
+                           paged_KV ? block_table.data_ptr() : nullptr,
+                           paged_KV ? (int)block_table.stride(0) : 0, page_block_size,
+                           alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs,
+                           max_seqlen_q, max_seqlen_k, total_q, batch_size, num_heads, num_heads_k,
+                           head_size, softmax_scale, window_size_left, window_size_right, softcap,
+                           q.dtype() == torch::kFloat16, cur_stream());
+        raise_if_failed("varlen_fwd");
+    } else {
+        out.zero_();
+        softmax_lse.fill_(std::numeric_limits<float>::infinity());
+    }
+    at::Tensor out_padded = out;
+    if (head_size_og % 8 != 0) out = out.index({"...", torch::indexing::Slice(torch::indexing::None, head_size_og)});
+    if (out_.has_value() && !out_.value().is_same(out)) out_.value().copy_(out), out = out_.value();
+    return {out, q_padded, k_padded, v_padded, out_padded, softmax_lse, p, rng_state};
+}
+
+std::vector<at::Tensor>
+mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcache,
+                c10::optional<const at::Tensor>& k_, c10::optional<const at::Tensor>& v_,
+                c10::optional<const at::Tensor>& seqlens_k_,
+                c10::optional<const at::Tensor>& rotary_cos_,
+                c10::optional<const at::Tensor>& rotary_sin_,
+                c10::optional<const at::Tensor>& cache_batch_idx_,
+                c10::optional<at::Tensor>& block_table_, c10::optional<at::Tensor>& alibi_slopes_,
+                c10::optional<at::Tensor>& out_, const float softmax_scale, bool is_causal,
+                int window_size_left, int window_size_right, const float softcap,
+                bool /*is_rotary_interleaved*/, int num_splits) {
+    check_qkv_dtype(q, kcache, vcache);
+    TORCH_CHECK(!k_.has_value() && !v_.has_value(),
+                "appending new K/V to the cache is not supported by this build");
+    TORCH_CHECK(!rotary_cos_.has_value() && !rotary_sin_.has_value(),
+                "rotary embedding on append is not supported by this build");
+    TORCH_CHECK(!cache_batch_idx_.has_value(), "cache_batch_idx is not supported by this build");
+    at::Tensor block_table;
+    const bool paged_KV = block_table_.has_value();
+    if (paged_KV) {
+        block_table = block_table_.value();
+        CHECK_DEVICE(block_table);
+        TORCH_CHECK(block_table.dtype() == torch::kInt32, "block_table must have dtype torch.int32");
+        TORCH_CHECK(block_table.stride(-1) == 1, "block_table must have contiguous last dimension");
+    }
+    const auto sizes = q.sizes();
+    const int batch_size = sizes[0];
+    const int seqlen_q = sizes[1];
+    const int num_heads = sizes[2];
+    const int head_size_og = sizes[3];
+    const int max_num_blocks_per_seq = !paged_KV ? 1 : block_table.size(1);
+    const int num_blocks = !paged_KV ? kcache.size(0) : kcache.size(0);
+    const int page_block_size = !paged_KV ? kcache.size(1) : kcache.size(1);
+    const int seqlen_k = max_num_blocks_per_seq * page_block_size;
+    const int num_heads_k = kcache.size(2);
+    TORCH_CHECK(batch_size > 0, "batch size must be positive");
+    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    if (seqlen_q == 1 && !alibi_slopes_.has_value()) is_causal = false;
+    if (is_causal) window_size_right = 0;
+    if (window_size_left >= seqlen_k) window_size_left = -1;
+    if (window_size_right >= seqlen_k) window_size_right = -1;
+    CHECK_SHAPE(q, batch_size, seqlen_q, num_heads, head_size_og);
+    if (!paged_KV) {
+        // Dense cache [batch, seqlen_k, hk, d]: one "page" per sequence (the reference's
+        // non-paged branch dereferences an undefined block_table, export.cpp:1711).
+        CHECK_SHAPE(kcache, batch_size, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(vcache, batch_size, page_block_size, num_heads_k, head_size_og);
+        block_table = torch::arange(batch_size, q.options().dtype(torch::kInt32)).view({batch_size, 1});
+    } else {
+        CHECK_SHAPE(kcache, num_blocks, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(vcache, num_blocks, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(block_table, batch_size, max_num_blocks_per_seq);
+    }
+    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
+    at::Tensor kc = pad_last(kcache, head_size_og).contiguous();
+    at::Tensor vc = pad_last(vcache, head_size_og).contiguous();
+    at::Tensor out;
+    if (out_.has_value()) {
+        out = out_.value();
+        TORCH_CHECK(out.dtype() == q.dtype(), "Output must have the same dtype as inputs");
+        CHECK_DEVICE(out);
+        TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
+        CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size_og);
+        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+    } else {
+        out = torch::empty_like(q_padded);
+    }
+    const int head_size = round8(head_size_og);
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto opts = q.options();
+    auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
+    at::Tensor seqlens;
+    if (seqlens_k_.has_value()) {
+        seqlens = seqlens_k_.value();
+        TORCH_CHECK(seqlens.dtype() == torch::kInt32, "seqlens_k must have dtype int32");
+        CHECK_DEVICE(seqlens);
+        CHECK_CONTIGUOUS(seqlens);
+        CHECK_SHAPE(seqlens, batch_size);
+    }
+    int64_t alibi_bs = 0;
+    at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
+    fmha_page_kvcache_fwd_ex(q_padded.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(),
+                             softmax_lse.data_ptr(), block_table.data_ptr(),
+                             (int)block_table.stride(0),
+                             seqlens.defined() ? seqlens.data_ptr() : nullptr, seqlen_q, seqlen_k,
+                             batch_size, num_heads, num_heads_k, head_size, page_block_size,
+                             softmax_scale, window_size_left, window_size_right, softcap,
+                             alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs,
+                             num_splits, 0, 1.f, 1.f, q.dtype() == torch::kFloat16, cur_stream());
+    raise_if_failed("fwd_kvcache");
+    if (head_size_og % 8 != 0) out = out.index({"...", torch::indexing::Slice(torch::indexing::None, head_size_og)});
+    if (out_.has_value() && !out_.value().is_same(out)) out_.value().copy_(out), out = out_.value();
+    return {out, softmax_lse};
+}
+
+std::vector<at::Tensor>
+mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+        const at::Tensor& out, const at::Tensor& softmax_lse, c10::optional<at::Tensor>& dq_,
+        c10::optional<at::Tensor>& dk_, c10::optional<at::Tensor>& dv_,
+        c10::optional<at::Tensor>& alibi_slopes_, const float p_dropout,
+        const float softmax_scale, const bool is_causal, int window_size_left,
+        int window_size_right, const float softcap, const bool deterministic,
+        c10::optional<at::Generator> /*gen_*/, c10::optional<at::Tensor>& /*rng_state*/) {
+    check_qkv_dtype(q, k, v);
+    if (is_causal) window_size_right = 0;
+    TORCH_CHECK(out.dtype() == q.dtype(), "query and out must have the same dtype");
+    TORCH_CHECK(dout.dtype() == q.dtype(), "query and dout must have the same dtype");
+    CHECK_DEVICE(out); CHECK_DEVICE(dout); CHECK_DEVICE(softmax_lse);
+    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    const auto sizes = q.sizes();
+    const int batch_size = sizes[0];
+    const int seqlen_q = sizes[1];
+    const int num_heads = sizes[2];
+    const int head_size_og = dout.size(3);
+    const int head_size = sizes[3];
+    const int seqlen_k = k.size(1);
+    const int num_heads_k = k.size(2);
+    TORCH_CHECK(batch_size > 0, "batch size must be positive");
+    TORCH_CHECK(head_size % 8 == 0, "head_size should be a multiple of 8");
+    TORCH_CHECK(head_size <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    TORCH_CHECK(head_size == round8(head_size_og), "head_size must be head_size_og rounded to a multiple of 8");
+    if (window_size_left >= seqlen_k) window_size_left = -1;
+    if (window_size_right >= seqlen_k) window_size_right = -1;
+    CHECK_SHAPE(q, batch_size, seqlen_q, num_heads, head_size);
+    CHECK_SHAPE(k, batch_size, seqlen_k, num_heads_k, head_size);
+    CHECK_SHAPE(v, batch_size, seqlen_k, num_heads_k, head_size);
+    CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size);
+    CHECK_SHAPE(dout, batch_size, seqlen_q, num_heads, head_size_og);
+    CHECK_SHAPE(softmax_lse, batch_size, num_heads, seqlen_q);
+    auto alloc = [&](c10::optional<at::Tensor>& t, const at::Tensor& like) {
+        if (t.has_value()) {
+            auto x = t.value();
+            TORCH_CHECK(x.dtype() == q.dtype(), "gradient must have the same dtype as q");
+            CHECK_DEVICE(x);
+            TORCH_CHECK(x.sizes() == like.sizes(), "gradient has the wrong shape");
+            if (x.is_contiguous()) return x;
+        }
+        return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
+    };
+    at::Tensor dq = alloc(dq_, q), dk = alloc(dk_, k), dv = alloc(dv_, v);
+    at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto opts = q.options();
+    auto softmax_d = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
+    int64_t alibi_bs = 0;
+    at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
+    auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
+    auto lse = softmax_lse.contiguous();
+    const size_t ws = fmha_bwd_workspace_size(seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, head_size);
+    at::Tensor workspace = torch::empty({(int64_t)ws}, opts.dtype(torch::kUInt8));
+    if (seqlen_q > 0) {
+        fmha_bwd(dout_padded.data_ptr(), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(), oc.data_ptr(),
+                 lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                 alibi.defined() ? alibi.data_ptr() : nullptr, softmax_d.data_ptr(), seqlen_q,
+                 seqlen_k, batch_size, num_heads, num_heads_k, head_size, p_dropout, softmax_scale,
+                 window_size_left, window_size_right, softcap, deterministic,
+                 q.dtype() == torch::kFloat16, cur_stream(), workspace.data_ptr(), ws);
+        raise_if_failed("bwd");
+    } else {
+        dk.zero_(); dv.zero_(); softmax_d.zero_();
+    }
+    auto fix = [&](c10::optional<at::Tensor>& t, at::Tensor& g) {
+        if (t.has_value() && !t.value().is_same(g)) { t.value().copy_(g); g = t.value(); }
+    };
+    fix(dq_, dq); fix(dk_, dk); fix(dv_, dv);
+    if (head_size_og % 8 != 0) {
+        using torch::indexing::Slice; using torch::indexing::None;
+        dq = dq.index({"...", Slice(None, head_size_og)});
+        dk = dk.index({"...", Slice(None, head_size_og)});
+        dv = dv.index({"...", Slice(None, head_size_og)});
+    }
+    return {dq, dk, dv, softmax_d};
+}
+
+std::vector<at::Tensor>
+mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+               const at::Tensor& v, const at::Tensor& out, const at::Tensor& softmax_lse,
+               c10::optional<at::Tensor>& dq_, c10::optional<at::Tensor>& dk_,
+               c10::optional<at::Tensor>& dv_, const at::Tensor& cu_seqlens_q,
+               const at::Tensor& cu_seqlens_k, c10::optional<at::Tensor>& alibi_slopes_,
+               const int max_seqlen_q, const int max_seqlen_k, const float p_dropout,
+               const float softmax_scale, const bool zero_tensors, const bool is_causal,
+               int window_size_left, int window_size_right, const float softcap,
+               const bool deterministic, c10::optional<at::Generator> /*gen_*/,
+               c10::optional<at::Tensor>& /*rng_state*/) {
+    check_qkv_dtype(q, k, v);
+    if (is_causal) window_size_right = 0;
+    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
+    TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
+    const int batch_size = cu_seqlens_q.numel() - 1;
+    const int total_q = q.size(0), num_heads = q.size(1), head_size = q.size(2);
+    const int total_k = k.size(0), num_heads_k = k.size(1);
+    const int head_size_og = dout.size(2);
+    TORCH_CHECK(head_size % 8 == 0 && head_size <= 128, "head_size must be a multiple of 8 and <= 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    if (window_size_left >= max_seqlen_k) window_size_left = -1;
+    if (window_size_right >= max_seqlen_k) window_size_right = -1;
+    CHECK_SHAPE(softmax_lse, num_heads, total_q);
+    auto alloc = [&](c10::optional<at::Tensor>& t, const at::Tensor& like) {
+        if (t.has_value() && t.value().is_contiguous()) return t.value();
+        return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
+    };
+    at::Tensor dq = alloc(dq_, q), dk = alloc(dk_, k), dv = alloc(dv_, v);
+    at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto opts = q.options();
+    auto softmax_d = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
+    int64_t alibi_bs = 0;
+    at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
+    auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
+    auto lse = softmax_lse.contiguous();
+    const size_t ws = fmha_varlen_bwd_workspace_size(total_q, total_k, batch_size, num_heads, num_heads_k, head_size);
+    at::Tensor workspace = torch::empty({(int64_t)ws}, opts.dtype(torch::kUInt8));
+    fmha_varlen_bwd(dout_padded.data_ptr(), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                    oc.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                    cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr(),
+                    alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs, max_seqlen_q,
+                    max_seqlen_k, total_q, total_k, batch_size, num_heads, num_heads_k, head_size,
+                    softmax_scale, window_size_left, window_size_right, softcap,
+                    q.dtype() == torch::kFloat16, cur_stream(), workspace.data_ptr(), ws);
+    raise_if_failed("varlen_bwd");
+    (void)zero_tensors; (void)deterministic;
+    if (head_size_og % 8 != 0) {
+        using torch::indexing::Slice; using torch::indexing::None;
+        dq = dq.index({"...", Slice(None, head_size_og)});
+        dk = dk.index({"...", Slice(None, head_size_og)});
+        dv = dv.index({"...", Slice(None, head_size_og)});
+    }
+    return {dq, dk, dv, softmax_d};
+}
+
+PYBIND11_MODULE(paged_attn, m) {
+    m.doc() = "FlashAttention for MI355X (gfx950): hand-written HIP kernels behind the paged_attn C ABI";
+    m.def("fwd", &mha_fwd, "Forward pass");
+    m.def("varlen_fwd", &mha_varlen_fwd, "Forward pass (variable length)");
+    m.def("fwd_kvcache", &mha_fwd_kvcache, "Forward pass, with KV-cache");
+    m.def("bwd", &mha_bwd, "Backward pass");
+    m.def("varlen_bwd", &mha_varlen_bwd, "Backward pass (variable length)");
+    m.def("version", []() { return std::string(fmha_version()); });
+}
