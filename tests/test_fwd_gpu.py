@@ -53,13 +53,21 @@ def test_fwd_golden(xfa, name):
     assert (lse.cpu()[fin] - lse_ref[fin]).abs().max().item() < LSE_ATOL
 
 
+def oracle_window(window, sk):
+    """API windows use -1 for 'unbounded'; the oracle's local branch (test.py:300-307) reads a
+    negative right window literally once the left one is set, so spell it out as sk there."""
+    wl, wr = window
+    return (wl, sk) if (wl >= 0 and wr < 0) else (wl, wr)
+
+
 def _rand_case(b, h, hk, sq, sk, d, dtype, causal, window=(-1, -1), seed=0):
     g = torch.Generator().manual_seed(seed)
     q = torch.randn(b, sq, h, d, generator=g).to(dtype)
     k = torch.randn(b, sk, hk, d, generator=g).to(dtype)
     v = torch.randn(b, sk, hk, d, generator=g).to(dtype)
-    out_ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
-    out_pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False,
+    w = oracle_window(window, sk)
+    out_ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=w)
+    out_pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=w, upcast=False,
                                   reorder_ops=True)
     return q, k, v, out_ref, out_pt
 

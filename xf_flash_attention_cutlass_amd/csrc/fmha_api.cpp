@@ -341,20 +341,132 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
 }
 
 
-// Backward entry points: filled in by the bwd milestone.
-size_t fmha_bwd_workspace_size(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t) { return 16; }
-size_t fmha_varlen_bwd_workspace_size(int32_t, int32_t, int32_t, int32_t, int32_t, int32_t) { return 16; }
-void fmha_bwd(void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, void*,
-              int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, float, float, int, int, float,
-              bool, bool, hipStream_t, void*, size_t) {
-    clear_error();
-    fail(4, "fmha_bwd: backward not available in this build");
+// ------------------------------------------------------------------ backward -----------
+static size_t bwd_ws_bytes(int64_t tokens, int h, int d) {
+    const int hd = hd_bucket(d);
+    const size_t acc = (size_t)tokens * h * hd * sizeof(float);
+    const size_t dsum = (size_t)tokens * h * sizeof(float);
+    return ((acc + 255) / 256) * 256 + ((dsum + 255) / 256) * 256;
 }
-void fmha_varlen_bwd(void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, void*,
-                     void*, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t, int32_t,
-                     int32_t, float, int, int, float, bool, hipStream_t, void*, size_t) {
-    clear_error();
-    fail(4, "fmha_varlen_bwd: backward not available in this build");
+
+size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t /*seqlen_k*/, int32_t batch_size,
+                               int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size) {
+    return bwd_ws_bytes((int64_t)batch_size * seqlen_q, num_heads, head_size);
+}
+
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t /*total_k*/, int32_t /*batch_size*/,
+                                      int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size) {
+    return bwd_ws_bytes(total_q, num_heads, head_size);
+}
+
+static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl, int wr,
+                       int seqlen_k_norm) {
+    set_windows(wl, wr, seqlen_k_norm);
+    p.wl = wl; p.wr = wr;
+    float scale_softmax = softmax_scale;
+    p.softcap_on = softcap > 0.f;
+    if (p.softcap_on) { p.softcap_pre = softmax_scale / softcap; scale_softmax = softcap; }
+    p.scale = softmax_scale;
+    p.scale_log2 = scale_softmax * 1.4426950408889634f;
+    p.alibi_mul = 1.f / scale_softmax;
+    return true;
+}
+
+void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse, void* dq,
+              void* dk, void* dv, void* alibi_slopes, void* softmax_d, int32_t seqlen_q,
+              int32_t seqlen_k, int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
+              int32_t head_size, float p_dropout, float softmax_scale, int window_size_left,
+              int window_size_right, float softcap, bool /*deterministic*/, bool is_fp16,
+              hipStream_t stream, void* workspace, size_t workspace_bytes) {
+    try {
+        clear_error();
+        if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
+        REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
+        REQUIRE(p_dropout == 0.f, "dropout is not supported by the backward (p_dropout=%g)", p_dropout);
+        const int h = num_heads, hk = num_heads_k, d = head_size;
+        const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d);
+        char* ws = (char*)workspace;
+        if (!ws) ws = (char*)pool_get(stream, need);
+        else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
+        REQUIRE(ws, "could not allocate %zu bytes of backward scratch", need);
+        const int hd = hd_bucket(d);
+        BwdParams p{};
+        p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout; p.lse = (const float*)softmax_lse;
+        p.dq = dq; p.dk = dk; p.dv = dv;
+        p.dq_accum = (float*)ws;
+        const size_t acc = (size_t)batch_size * seqlen_q * h * hd * sizeof(float);
+        p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + ((acc + 255) / 256) * 256);
+        p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = (int64_t)seqlen_q * h * d;
+        p.o_row = p.q_row; p.o_head = d; p.o_batch = p.q_batch;
+        p.do_row = p.q_row; p.do_head = d; p.do_batch = p.q_batch;
+        p.dq_row = p.q_row; p.dq_head = d; p.dq_batch = p.q_batch;
+        p.k_row = (int64_t)hk * d; p.k_head = d; p.k_batch = (int64_t)seqlen_k * hk * d;
+        p.v_row = p.k_row; p.v_head = d; p.v_batch = p.k_batch;
+        p.dk_row = p.k_row; p.dk_head = d; p.dk_batch = p.k_batch;
+        p.dv_row = p.k_row; p.dv_head = d; p.dv_batch = p.k_batch;
+        p.lse_batch = (int64_t)h * seqlen_q; p.lse_head = seqlen_q;
+        p.acc_row = hd; p.acc_head = (int64_t)seqlen_q * hd; p.acc_batch = (int64_t)h * seqlen_q * hd;
+        p.alibi = (const float*)alibi_slopes;
+        p.alibi_bstride = batch_size > 1 ? num_heads : 0;
+        p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
+        p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
+        bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, seqlen_k);
+        hip_ok(dispatch_bwd(p, !is_fp16, stream), "backward launch");
+    } catch (...) {
+        fail(9, "internal error in fmha_bwd");
+    }
+}
+
+void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
+                     void* dq, void* dk, void* dv, void* cu_seqlens_q, void* cu_seqlens_k,
+                     void* alibi_slopes, int32_t alibi_batch_stride, int32_t max_seqlen_q,
+                     int32_t max_seqlen_k, int32_t total_q, int32_t total_k,
+                     int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
+                     int32_t head_size, float softmax_scale, int window_size_left,
+                     int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
+                     void* workspace, size_t workspace_bytes) {
+    try {
+        clear_error();
+        if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
+        REQUIRE(cu_seqlens_q && cu_seqlens_k, "cu_seqlens_q/cu_seqlens_k must be non-null");
+        REQUIRE(total_q > 0 && total_k > 0 && max_seqlen_q > 0 && max_seqlen_k > 0,
+                "total/max sequence lengths must be positive");
+        const int h = num_heads, hk = num_heads_k, d = head_size;
+        const size_t need = bwd_ws_bytes(total_q, h, d);
+        char* ws = (char*)workspace;
+        if (!ws) ws = (char*)pool_get(stream, need);
+        else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
+        REQUIRE(ws, "could not allocate %zu bytes of backward scratch", need);
+        const int hd = hd_bucket(d);
+        BwdParams p{};
+        p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout; p.lse = (const float*)softmax_lse;
+        p.dq = dq; p.dk = dk; p.dv = dv;
+        p.dq_accum = (float*)ws;
+        const size_t acc = (size_t)total_q * h * hd * sizeof(float);
+        p.dsum = (float*)(ws + ((acc + 255) / 256) * 256);
+        p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
+        p.o_row = p.q_row; p.o_head = d; p.o_batch = 0;
+        p.do_row = p.q_row; p.do_head = d; p.do_batch = 0;
+        p.dq_row = p.q_row; p.dq_head = d; p.dq_batch = 0;
+        p.k_row = (int64_t)hk * d; p.k_head = d; p.k_batch = 0;
+        p.v_row = p.k_row; p.v_head = d; p.v_batch = 0;
+        p.dk_row = p.k_row; p.dk_head = d; p.dk_batch = 0;
+        p.dv_row = p.k_row; p.dv_head = d; p.dv_batch = 0;
+        p.lse_batch = 0; p.lse_head = total_q;                 // LSE [h, total_q]
+        p.acc_row = hd; p.acc_head = (int64_t)total_q * hd; p.acc_batch = 0;
+        p.cu_seqlens_q = (const int*)cu_seqlens_q;
+        p.cu_seqlens_k = (const int*)cu_seqlens_k;
+        p.alibi = (const float*)alibi_slopes;
+        p.alibi_bstride = alibi_batch_stride;
+        p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
+        p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
+        bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, max_seqlen_k);
+        hip_ok(dispatch_bwd(p, !is_fp16, stream), "varlen backward launch");
+    } catch (...) {
+        fail(9, "internal error in fmha_varlen_bwd");
+    }
 }
 
 }  // extern "C"

@@ -1,4 +1,7 @@
-// fmha_bwd.hip — backward instantiations (placeholder until the bwd kernels land).
+// fmha_bwd.hip — backward instantiations for one (head dim, dtype) pair (see fmha_fwd.hip).
+// Launch sequence replaces run_flash_bwd_seqk_parallel (flash_bwd_launch_template_hip.h:76-136):
+// preprocess (D = rowsum(dO*O), zero dQaccum) -> main (dK, dV, dQaccum) -> convert dQ.
+#include "fmha_bwd_kernel.h"
 #include "fmha_launch.h"
 
 #define XFA_CAT2(a, b) a##b
@@ -6,5 +9,47 @@
 #define XFA_FN(hd, dt) XFA_CAT(XFA_CAT(XFA_CAT(launch_bwd_hd, hd), _), dt)
 
 namespace xfa {
-hipError_t XFA_FN(XFA_HD, XFA_DTN)(const BwdParams&, hipStream_t) { return hipErrorNotSupported; }
+
+#if XFA_DT_BF16
+typedef __bf16 elem_t;
+#else
+typedef _Float16 elem_t;
+#endif
+
+template <int HD, typename T>
+static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
+    const int64_t tokens = p.cu_seqlens_q ? (p.acc_head / p.acc_row) : (int64_t)p.b * p.seqlen_q;
+    const int total_rows = (int)(tokens * p.h);
+    const int64_t threads = (int64_t)total_rows * (HD / 8);
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    hipLaunchKernelGGL((fmha_bwd_pre_kernel<HD, T>), dim3(blocks), dim3(256), 0, st, p, total_rows);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+
+    const bool mask = p.wl >= 0 || p.wr >= 0;
+    const bool feat = p.alibi || p.softcap_on || p.cu_seqlens_q || p.cu_seqlens_k;
+    void (*kern)(const BwdParams) =
+        mask ? (feat ? fmha_bwd_kernel<HD, T, true, true> : fmha_bwd_kernel<HD, T, true, false>)
+             : (feat ? fmha_bwd_kernel<HD, T, false, true> : fmha_bwd_kernel<HD, T, false, false>);
+    const size_t smem = 2 * (size_t)kBwdBlockN * HD * 2 + 2 * (size_t)kBwdBlockM * HD * 2 + kBwdBlockN * 64;
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        attr_done = true;
+    }
+    const dim3 grid(p.b * p.hk, (p.seqlen_k + kBwdBlockN - 1) / kBwdBlockN);
+    hipLaunchKernelGGL(kern, grid, dim3(kBwdWaves * 64), smem, st, p);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((fmha_bwd_convert_kernel<HD, T>), dim3(blocks), dim3(256), 0, st, p, total_rows);
+    return hipGetLastError();
+}
+
+hipError_t XFA_FN(XFA_HD, XFA_DTN)(const BwdParams& p, hipStream_t st) {
+    return launch_bwd_impl<XFA_HD, elem_t>(p, st);
+}
+
 }  // namespace xfa

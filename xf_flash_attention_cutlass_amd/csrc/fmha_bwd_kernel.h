@@ -1,0 +1,431 @@
+// fmha_bwd_kernel.h — flash-attention backward for gfx950 (CDNA4).
+//
+// The reference ships the backward only as unbuilt code: bwd preprocess `compute_dot_do_o`
+// (flash_bwd_preprocess_kernel_hip.h:59-141), main `compute_dq_dk_dv_1colblock`
+// (flash_bwd_kernel_hip.h:89-724, seqk-parallel driver :755-767, fp32 dQ atomics :637),
+// `convert_dQ` (flash_bwd_preprocess_kernel_hip.h:184-270) and host-side GQA reduction
+// (export.cpp:1165-1168).  Same math here, re-designed for CDNA4:
+//
+//  * one workgroup = 4 waves (one per SIMD, the whole 512-entry register file each) = 256 keys
+//    of one (batch, kv-head); each wave owns 64 keys and keeps dK^T and dV^T of them in
+//    (accumulation) registers while the workgroup sweeps every query head of the GQA group x
+//    32-row query tiles — dK/dV need no cross-workgroup (or host) reduction;
+//  * key-on-the-lane orientation: S = Q K^T and dP = dO V^T land with the key on the MFMA
+//    lane, so (after a pairwise cvt) P and dS are directly the B operands of
+//    dV^T += dO^T P and dK^T += Q^T dS (v_mfma_f32_32x32x16); dO^T / Q^T come from the same
+//    swizzled LDS tile through ds_read_b64_tr_b16;
+//  * dS crosses LDS once (as dS^T, bf16) for dQ = dS K, computed with v_mfma_f32_16x16x32 by
+//    all waves and added to an fp32 dQ accumulator with global float atomics (256 keys per
+//    workgroup => 640 MFMA flops per atomic byte, cdna_hip_programming.md Appendix B);
+//  * P is recomputed from the forward LSE; D = rowsum(dO*O) comes from the preprocess kernel.
+#pragma once
+
+#include "fmha_common.h"
+
+namespace xfa {
+
+constexpr int kBwdWaves = 4;                 // waves per workgroup (one per SIMD)
+constexpr int kBwdKeysPerWave = 64;          // keys owned by one wave (2 x 32-key subtiles)
+constexpr int kBwdBlockN = kBwdKeysPerWave * kBwdWaves;   // keys per workgroup
+constexpr int kBwdBlockM = 32;               // query rows per tile
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+template <typename T> struct DT16;
+template <> struct DT16<__bf16> {
+    static __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct DT16<_Float16> {
+    static __device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// dS^T tile [256 keys][32 q] bf16, 64-byte rows: XOR the 16-byte chunk with bit 3 of the row
+// so the two 4-row blocks one tr-read half touches (8 rows apart) use different banks.
+__device__ __forceinline__ int ds_off(int row, int col) {
+    return row * 64 + ((((col >> 3) ^ (((row >> 3) & 1) << 1))) << 4) + ((col >> 2) & 1) * 8;
+}
+
+// ---------------------------------------------------------------- preprocess ---------------
+// D[row] = sum_d dO*O (fp32), and zero the fp32 dQ accumulator row.
+template <int HD, typename T>
+__global__ void __launch_bounds__(256) fmha_bwd_pre_kernel(const BwdParams p, int total_rows) {
+    constexpr int TPR = HD / 8;                 // threads per (token, head) row
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int r = t / TPR;
+    const int c = t % TPR;
+    if (r >= total_rows) return;
+    const int head = r % p.h;
+    const int tok = r / p.h;                    // dense: b*sq + pos ; varlen: global token
+    int bidx, pos;
+    if (p.cu_seqlens_q) { bidx = 0; pos = tok; }
+    else { bidx = tok / p.seqlen_q; pos = tok - bidx * p.seqlen_q; }
+    const int d0 = c * 8;
+    float acc = 0.f;
+    if (d0 < p.d) {
+        const T* o = reinterpret_cast<const T*>(p.o) + (int64_t)bidx * p.o_batch + (int64_t)pos * p.o_row +
+                     (int64_t)head * p.o_head + d0;
+        const T* g = reinterpret_cast<const T*>(p.dout) + (int64_t)bidx * p.do_batch +
+                     (int64_t)pos * p.do_row + (int64_t)head * p.do_head + d0;
+        typedef __attribute__((ext_vector_type(8))) T T8;
+        const T8 ov = *reinterpret_cast<const T8*>(o);
+        const T8 gv = *reinterpret_cast<const T8*>(g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = fmaf((float)ov[j], (float)gv[j], acc);
+    }
+#pragma unroll
+    for (int m = TPR / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+    const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + pos;
+    if (c == 0) p.dsum[li] = acc;
+    float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+                (int64_t)pos * p.acc_row + d0;
+    *reinterpret_cast<f32x4_t*>(qa) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4_t*>(qa + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+}
+
+// dQ = dQaccum * scale -> dtype
+template <int HD, typename T>
+__global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p, int total_rows) {
+    constexpr int TPR = HD / 8;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int r = t / TPR;
+    const int c = t % TPR;
+    if (r >= total_rows) return;
+    const int head = r % p.h;
+    const int tok = r / p.h;
+    int bidx, pos;
+    if (p.cu_seqlens_q) { bidx = 0; pos = tok; }
+    else { bidx = tok / p.seqlen_q; pos = tok - bidx * p.seqlen_q; }
+    const int d0 = c * 8;
+    if (d0 >= p.d) return;
+    const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+                      (int64_t)pos * p.acc_row + d0;
+    typedef __attribute__((ext_vector_type(8))) T T8;
+    T8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (T)(qa[j] * p.scale);
+    T* dq = reinterpret_cast<T*>(p.dq) + (int64_t)bidx * p.dq_batch + (int64_t)pos * p.dq_row +
+            (int64_t)head * p.dq_head + d0;
+    *reinterpret_cast<T8*>(dq) = v;
+}
+
+// ---------------------------------------------------------------- main ---------------------
+template <int HD, typename T, bool MASK, bool FEAT>
+__global__ void __launch_bounds__(kBwdWaves * 64, 1) fmha_bwd_kernel(const BwdParams p) {
+    using V8 = typename DT<T>::v8;
+    constexpr int NW = kBwdWaves;
+    constexpr int NT = NW * 64;
+    constexpr int KS = kBwdKeysPerWave / 32;     // 32-key subtiles per wave
+    constexpr int BN = kBwdBlockN;
+    constexpr int BQ = kBwdBlockM;
+    constexpr int CPR = HD / 8;
+    constexpr int NS = HD / 16;
+    constexpr int ND = HD / 32;
+    constexpr int KT_BYTES = BN * HD * 2;
+    constexpr int QT_BYTES = BQ * HD * 2;
+    constexpr int NDQ = (HD / 16) / (NW / 2);   // 16x16 dQ tiles per wave (2 query halves)
+    constexpr int QLD = BQ * CPR / NT;          // Q (and dO) chunks per thread
+    static_assert(QLD >= 1 && BQ * CPR == QLD * NT, "Q/dO tile geometry");
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* k_lds = smem;
+    char* v_lds = smem + KT_BYTES;
+    char* q_lds = v_lds + KT_BYTES;
+    char* do_lds = q_lds + QT_BYTES;
+    char* ds_lds = do_lds + QT_BYTES;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int lr = lane & 31;
+    const int hh = lane >> 5;
+
+    const int bh = blockIdx.x;
+    const int bidx = bh / p.hk;
+    const int hk_i = bh - bidx * p.hk;
+    const int n0 = blockIdx.y * BN;
+
+    int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
+    if (FEAT) {
+        if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
+        if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
+    }
+    if (n0 >= sk) return;
+    const int diag = sk - sq;
+
+    // query positions that can see any key of [n0, n0 + BN)
+    int p_lo = 0, p_hi = sq;
+    if (MASK && p.wr >= 0) p_lo = max(0, n0 - diag - p.wr);
+    if (MASK && p.wl >= 0) p_hi = min(sq, n0 + BN - 1 - diag + p.wl + 1);
+    const int t_lo = p_lo / BQ;
+    const int ntiles = p_hi > p_lo ? (p_hi + BQ - 1) / BQ - t_lo : 0;
+    const int G = p.group;
+    const int n_iter = ntiles * G;
+
+    // ---- K and V tiles (all BN keys) -> LDS, once
+    {
+        const T* kb = reinterpret_cast<const T*>(p.k) + (int64_t)bidx * p.k_batch +
+                      (int64_t)k_off * p.k_row + (int64_t)hk_i * p.k_head;
+        const T* vb = reinterpret_cast<const T*>(p.v) + (int64_t)bidx * p.v_batch +
+                      (int64_t)k_off * p.v_row + (int64_t)hk_i * p.v_head;
+        for (int i = tid; i < BN * CPR; i += NT) {
+            const int r = i / CPR, c = i % CPR;
+            const int n = n0 + r;
+            uint4 x = make_uint4(0, 0, 0, 0), y = make_uint4(0, 0, 0, 0);
+            if (n < sk && c * 8 < p.d) {
+                x = *reinterpret_cast<const uint4*>(kb + (int64_t)n * p.k_row + c * 8);
+                y = *reinterpret_cast<const uint4*>(vb + (int64_t)n * p.v_row + c * 8);
+            }
+            *reinterpret_cast<uint4*>(k_lds + lds_off<HD>(r, c)) = x;
+            *reinterpret_cast<uint4*>(v_lds + lds_off<HD>(r, c)) = y;
+        }
+    }
+    int my_key[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) my_key[ks] = n0 + wave * kBwdKeysPerWave + 32 * ks + lr;
+
+    // ---- Q / dO tile loader (QLD 16-byte chunks of each per thread)
+    const int lrow = tid / CPR, lcol = tid % CPR;
+    constexpr int LROW_STEP = NT / CPR;
+    const bool ld_ok = lcol * 8 < p.d;
+    uint4 qreg[QLD], doreg[QLD];
+    auto load_q = [&](int it) {
+        const int g = it / ntiles;
+        const int tt = it - g * ntiles;
+        const int head = hk_i * G + g;
+#pragma unroll
+        for (int i = 0; i < QLD; ++i) {
+            const int pos = (t_lo + tt) * BQ + lrow + i * LROW_STEP;
+            qreg[i] = make_uint4(0, 0, 0, 0);
+            doreg[i] = make_uint4(0, 0, 0, 0);
+            if (ld_ok && pos < sq) {
+                const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
+                              (int64_t)(q_off + pos) * p.q_row + (int64_t)head * p.q_head + lcol * 8;
+                const T* gp = reinterpret_cast<const T*>(p.dout) + (int64_t)bidx * p.do_batch +
+                              (int64_t)(q_off + pos) * p.do_row + (int64_t)head * p.do_head + lcol * 8;
+                qreg[i] = *reinterpret_cast<const uint4*>(qp);
+                doreg[i] = *reinterpret_cast<const uint4*>(gp);
+            }
+        }
+    };
+    auto store_q = [&]() {
+#pragma unroll
+        for (int i = 0; i < QLD; ++i) {
+            const int r = lrow + i * LROW_STEP;
+            *reinterpret_cast<uint4*>(q_lds + lds_off<HD>(r, lcol)) = qreg[i];
+            *reinterpret_cast<uint4*>(do_lds + lds_off<HD>(r, lcol)) = doreg[i];
+        }
+    };
+
+    // per-lane LDS offsets
+    int koff[NS], qoff[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        koff[s] = lds_off<HD>(wave * kBwdKeysPerWave + lr, 2 * s + hh);   // + 32*ks rows
+        qoff[s] = lds_off<HD>(lr, 2 * s + hh);
+    }
+    const int q4 = (lane & 15) >> 2;
+    int troff[2][ND];   // transposed reads of the Q / dO tile (A operand: rows q, column d)
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+            const int r = 4 * hh + q4 + 8 * part;
+            const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            troff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+        }
+    // dQ phase (16x16x32): wave -> query half mt, d tiles
+    const int mt = wave & 1;
+    const int g16 = lane >> 4;
+    const int p4 = lane & 3;
+    const int qq = (lane & 15) >> 2;
+    // tr-read bases for dQ = dS K; the swizzles only see row bits < 4, so the 32-key step
+    // is a plain immediate offset (keeps the addresses out of the register budget)
+    int dq_aoff[2], dq_boff[NDQ][2];
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+        const int kr0 = 8 * g16 + qq + 4 * part;
+        dq_aoff[part] = ds_off(kr0, 16 * mt + 4 * p4);
+#pragma unroll
+        for (int i = 0; i < NDQ; ++i) {
+            const int dcol = 16 * ((wave >> 1) * NDQ + i) + 4 * p4;
+            dq_boff[i][part] = lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
+        }
+    }
+
+    f32x16 dk[KS][ND], dv[KS][ND];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
+
+    const float c = p.scale_log2;
+    if (n_iter > 0) { load_q(0); }
+    __syncthreads();                     // K tile visible
+    if (n_iter > 0) { store_q(); }
+    __syncthreads();
+
+    for (int it = 0; it < n_iter; ++it) {
+        const int g = it / ntiles;
+        const int tt = it - g * ntiles;
+        const int head = hk_i * G + g;
+        const int q0 = (t_lo + tt) * BQ;
+        if (it + 1 < n_iter) load_q(it + 1);
+
+        // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
+        f32x16 s_acc[KS], dp_acc[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) { s_acc[ks] = f32x16{}; dp_acc[ks] = f32x16{}; }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const V8 qa = *reinterpret_cast<const V8*>(q_lds + qoff[s]);
+            const V8 ga = *reinterpret_cast<const V8*>(do_lds + qoff[s]);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const V8 kb = *reinterpret_cast<const V8*>(k_lds + ks * 32 * HD * 2 + koff[s]);
+                const V8 vb = *reinterpret_cast<const V8*>(v_lds + ks * 32 * HD * 2 + koff[s]);
+                s_acc[ks] = DT<T>::mfma32(qa, kb, s_acc[ks]);
+                dp_acc[ks] = DT<T>::mfma32(ga, vb, dp_acc[ks]);
+            }
+        }
+        // ---- P = exp2(S*c - LSE*log2e), dS = P * (dP - D)
+        const int64_t lrow_base = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off;
+        float alibi_w = 0.f;
+        if (FEAT && p.alibi) alibi_w = p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+            const int pos0 = q0 + 8 * gq + 4 * hh;
+            float lse4[4], d4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool ok = pos0 + i < sq;
+                lse4[i] = ok ? p.lse[lrow_base + pos0 + i] * kLog2e : INFINITY;
+                d4[i] = ok ? p.dsum[lrow_base + pos0 + i] : 0.f;
+            }
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 4 * gq + i;
+                const int pos = pos0 + i;
+                const int key = my_key[ks];
+                float w = s_acc[ks][r];
+                float dcap = 1.f;
+                if (FEAT && p.softcap_on) { w = fast_tanh(w * p.softcap_pre); dcap = 1.f - w * w; }
+                if (FEAT && p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
+                float pr = fast_exp2(fmaf(w, c, -lse4[i]));
+                bool keep = key < sk;
+                if (MASK) {
+                    if (p.wr >= 0) keep = keep && key < pos + diag + p.wr + 1;
+                    if (p.wl >= 0) keep = keep && key >= pos + diag - p.wl;
+                }
+                pr = keep ? pr : 0.f;
+                s_acc[ks][r] = pr;
+                dp_acc[ks][r] = pr * (dp_acc[ks][r] - d4[i]) * dcap;
+            }
+        }
+        // ---- dV^T += dO^T P ; dK^T += Q^T dS  (P / dS accumulators are the B operands)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+            const int rb = 16 * sp * HD * 2;
+#pragma unroll
+            for (int dt = 0; dt < ND; ++dt) {
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff[0][dt]));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff[1][dt]));
+                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff[0][dt]));
+                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff[1][dt]));
+                const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    V8 pb, sb;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { pb[j] = (T)s_acc[ks][8 * sp + j]; sb[j] = (T)dp_acc[ks][8 * sp + j]; }
+                    dv[ks][dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb, dv[ks][dt]);
+                    dk[ks][dt] = DT<T>::mfma32(__builtin_bit_cast(V8, bv), sb, dk[ks][dt]);
+                }
+            }
+        }
+        // ---- dS^T -> LDS (bf16/f16): row = key (this lane), 4 consecutive q per store
+        {
+            typedef __attribute__((ext_vector_type(4))) T T4;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int krow = wave * kBwdKeysPerWave + 32 * ks + lr;
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const T4 v = {(T)dp_acc[ks][4 * gq], (T)dp_acc[ks][4 * gq + 1],
+                                  (T)dp_acc[ks][4 * gq + 2], (T)dp_acc[ks][4 * gq + 3]};
+                    *reinterpret_cast<T4*>(ds_lds + ds_off(krow, 8 * gq + 4 * hh)) = v;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- dQ[q][d] += dS K over the 256 keys (16x16x32; A = dS via tr-read of dS^T)
+        {
+            f32x4 dq[NDQ];
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i) dq[i] = f32x4{};
+#pragma unroll
+            for (int ks = 0; ks < BN / 32; ++ks) {
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 32 * 64 + dq_aoff[0]));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 32 * 64 + dq_aoff[1]));
+                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const V8 a = __builtin_bit_cast(V8, av);
+#pragma unroll
+                for (int i = 0; i < NDQ; ++i) {
+                    const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dq_boff[i][0]));
+                    const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dq_boff[i][1]));
+                    const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                    dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
+                }
+            }
+            float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head;
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i) {
+                const int d = 16 * ((wave >> 1) * NDQ + i) + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int pos = q0 + 16 * mt + 4 * g16 + r;
+                    if (pos < sq && d < p.d)
+                        atomicAdd(qa + (int64_t)(q_off + pos) * p.acc_row + d, dq[i][r]);
+                }
+            }
+        }
+        if (it + 1 < n_iter) store_q();
+        __syncthreads();
+    }
+
+    // ---- epilogue: dK = scale * (dK^T)^T, dV = (dV^T)^T
+    typedef __attribute__((ext_vector_type(4))) T T4;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int key = my_key[ks];
+        if (key >= sk) continue;
+        T* dkr = reinterpret_cast<T*>(p.dk) + (int64_t)bidx * p.dk_batch + (int64_t)(k_off + key) * p.dk_row +
+                 (int64_t)hk_i * p.dk_head;
+        T* dvr = reinterpret_cast<T*>(p.dv) + (int64_t)bidx * p.dv_batch + (int64_t)(k_off + key) * p.dv_row +
+                 (int64_t)hk_i * p.dv_head;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int d = 32 * dt + 8 * gq + 4 * hh;
+                if (d < p.d) {
+                    const T4 kv = {(T)(dk[ks][dt][4 * gq] * p.scale), (T)(dk[ks][dt][4 * gq + 1] * p.scale),
+                                   (T)(dk[ks][dt][4 * gq + 2] * p.scale), (T)(dk[ks][dt][4 * gq + 3] * p.scale)};
+                    const T4 vv = {(T)dv[ks][dt][4 * gq], (T)dv[ks][dt][4 * gq + 1],
+                                   (T)dv[ks][dt][4 * gq + 2], (T)dv[ks][dt][4 * gq + 3]};
+                    *reinterpret_cast<T4*>(dkr + d) = kv;
+                    *reinterpret_cast<T4*>(dvr + d) = vv;
+                }
+            }
+    }
+}
+
+}  // namespace xfa
