@@ -145,7 +145,8 @@ def main():
     allgather = None
     if dist:
         # RCCL all-gather of every rank's O shard over xGMI (assembling the sharded output).
-        gathered = torch.empty((world,) + tuple(out.shape), device=dev, dtype=out.dtype)
+        gathered = torch.empty((world * out.shape[0],) + tuple(out.shape[1:]), device=dev,
+                               dtype=out.dtype)
         for _ in range(3):
             dist.all_gather_into_tensor(gathered, out)
         torch.cuda.synchronize()

@@ -1,0 +1,158 @@
+"""Multi-GPU sharding of the attention hot path (one process per GPU, torch.distributed).
+
+The reference has no distributed code (no NCCL/RCCL call sites).  Attention has
+no reduction across (batch, head) units in the forward, so the units are partitioned across
+ranks and every rank runs the single-GPU kernels on its shard with NO collective in the data
+path; the only exchange is an optional all-gather (RCCL over xGMI on MI355X, `nccl` backend =
+RCCL) that assembles the sharded outputs on every rank:
+
+  * dense fwd/bwd (C2/C3)  : shard heads in contiguous, GQA-aligned ranges (a K/V head and all
+                             query heads that read it stay on one rank, so dK/dV need no
+                             cross-rank reduction); fall back to batch shards when hk < world;
+  * varlen (C4)            : shard whole sequences, greedy-balanced on sum(s_q * s_k);
+  * paged decode (C5)      : shard the batch; every rank owns its sequences' pages, no KV moves.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Sequence, Tuple
+
+import torch
+
+
+@dataclass(frozen=True)
+class Shard:
+    start: int
+    stop: int
+
+    @property
+    def size(self) -> int:
+        return self.stop - self.start
+
+
+def even_ranges(n: int, world: int) -> List[Shard]:
+    """Split range(n) into `world` contiguous chunks whose sizes differ by at most one."""
+    base, rem = divmod(n, world)
+    out, s = [], 0
+    for r in range(world):
+        e = s + base + (1 if r < rem else 0)
+        out.append(Shard(s, e))
+        s = e
+    return out
+
+
+def head_shards(num_heads: int, num_heads_k: int, world: int) -> List[Tuple[Shard, Shard]]:
+    """GQA-aligned head ranges: rank r gets kv heads [a, b) and query heads [a*G, b*G)."""
+    if num_heads % num_heads_k:
+        raise ValueError("num_heads must be a multiple of num_heads_k")
+    if num_heads_k < world:
+        raise ValueError(f"cannot shard {num_heads_k} kv heads over {world} ranks; use batch shards")
+    g = num_heads // num_heads_k
+    return [(Shard(s.start * g, s.stop * g), s) for s in even_ranges(num_heads_k, world)]
+
+
+def balanced_sequences(seqlens_q: Sequence[int], seqlens_k: Sequence[int], world: int) -> List[List[int]]:
+    """Greedy longest-processing-time assignment of whole sequences on cost s_q * s_k."""
+    cost = [int(a) * int(b) for a, b in zip(seqlens_q, seqlens_k)]
+    order = sorted(range(len(cost)), key=lambda i: -cost[i])
+    load = [0] * world
+    parts: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda j: (load[j], j))
+        parts[r].append(i)
+        load[r] += cost[i]
+    return [sorted(p) for p in parts]
+
+
+def _world():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist, dist.get_rank(), dist.get_world_size()
+    return None, 0, 1
+
+
+def all_gather_heads(local: torch.Tensor, shards: List[Tuple[Shard, Shard]], head_dim: int = 2):
+    """Assemble [b, s, H, d] from per-rank head shards [b, s, H_r, d] (all ranks get the full
+    tensor).  Uneven shards are padded to the largest for one all_gather_into_tensor."""
+    dist, rank, world = _world()
+    if world == 1:
+        return local
+    hmax = max(q.size for q, _ in shards)
+    pad = list(local.shape)
+    pad[head_dim] = hmax
+    buf = local.new_zeros(pad)
+    buf.narrow(head_dim, 0, local.shape[head_dim]).copy_(local)
+    gathered = local.new_empty([world * pad[0]] + pad[1:])     # rank-major concatenation
+    dist.all_gather_into_tensor(gathered, buf.contiguous())
+    gathered = gathered.view([world] + pad)
+    pieces = [gathered[r].narrow(head_dim, 0, shards[r][0].size) for r in range(world)]
+    return torch.cat(pieces, dim=head_dim)
+
+
+def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                      local_fn: Callable | None = None, gather: bool = True, **kw):
+    """Head-sharded attention: every rank holds the full (replicated) q/k/v views, computes
+    its GQA-aligned head range with `local_fn` (default: the gfx950 kernels) and, if `gather`,
+    all-gathers the outputs.  Returns (out, my_query_head_shard)."""
+    dist, rank, world = _world()
+    if local_fn is None:
+        from . import flash_attn_func as local_fn
+    shards = head_shards(q.shape[2], k.shape[2], world)
+    qs, ks = shards[rank]
+    out_local = local_fn(q[:, :, qs.start:qs.stop].contiguous(),
+                         k[:, :, ks.start:ks.stop].contiguous(),
+                         v[:, :, ks.start:ks.stop].contiguous(), **kw)
+    if not gather:
+        return out_local, qs
+    return all_gather_heads(out_local, shards), qs
+
+
+def sharded_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, local_fn: Callable | None = None,
+                   gather: bool = True, **kw):
+    """Sequence-sharded varlen attention (C4): ranks take whole sequences, balanced on
+    s_q*s_k; outputs are all-gathered back into the packed [total_q, H, d] order."""
+    dist, rank, world = _world()
+    if local_fn is None:
+        from . import flash_attn_varlen_func as local_fn
+    cq = [int(x) for x in cu_seqlens_q.tolist()]
+    ck = [int(x) for x in cu_seqlens_k.tolist()]
+    lq = [b - a for a, b in zip(cq[:-1], cq[1:])]
+    lk = [b - a for a, b in zip(ck[:-1], ck[1:])]
+    parts = balanced_sequences(lq, lk, world)
+    mine = parts[rank]
+    dev = q.device
+    if mine:
+        qi = torch.cat([torch.arange(cq[i], cq[i + 1]) for i in mine]).to(dev)
+        ki = torch.cat([torch.arange(ck[i], ck[i + 1]) for i in mine]).to(dev)
+        cql = torch.tensor([0] + list(torch.tensor([lq[i] for i in mine]).cumsum(0).tolist()),
+                           dtype=torch.int32, device=dev)
+        ckl = torch.tensor([0] + list(torch.tensor([lk[i] for i in mine]).cumsum(0).tolist()),
+                           dtype=torch.int32, device=dev)
+        out_local = local_fn(q[qi], k[ki], v[ki], cql, ckl, max(lq[i] for i in mine),
+                             max(lk[i] for i in mine), **kw)
+    else:
+        qi = torch.empty(0, dtype=torch.long, device=dev)
+        out_local = q.new_empty((0,) + tuple(q.shape[1:]))
+    if not gather or world == 1:
+        return out_local, qi
+    # pad to the largest local token count, gather, then scatter back into packed order
+    n_local = torch.tensor([out_local.shape[0]], device=dev)
+    counts = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(counts, n_local)
+    nmax = int(max(c.item() for c in counts))
+    buf = q.new_zeros((nmax,) + tuple(q.shape[1:]))
+    buf[: out_local.shape[0]] = out_local
+    gathered = q.new_empty((world * nmax,) + tuple(q.shape[1:]))
+    dist.all_gather_into_tensor(gathered, buf)
+    gathered = gathered.view((world, nmax) + tuple(q.shape[1:]))
+    out = q.new_empty(q.shape)
+    for r in range(world):
+        idx = torch.cat([torch.arange(cq[i], cq[i + 1]) for i in parts[r]]).to(dev) if parts[r] \
+            else torch.empty(0, dtype=torch.long, device=dev)
+        out[idx] = gathered[r, : idx.numel()]
+    return out, qi
+
+
+def batch_shards(batch: int, world: int) -> List[Shard]:
+    """Paged decode (C5): contiguous batch ranges; each rank owns its sequences' KV pages."""
+    return even_ranges(batch, world)
