@@ -86,6 +86,11 @@ int fmha_last_status(void);
 /* Library version / build identification, e.g. "xf-fmha-gfx950 1.0". */
 const char* fmha_version(void);
 
+/* Process-wide tuning knobs (not thread-safe against concurrent launches).  Returns 0, or -1
+ * for an unknown name / invalid value.  "fwd_waves": 4 or 8 waves (128 / 256 query rows) per
+ * forward workgroup. */
+int fmha_set_option(const char* name, int value);
+
 /* Varlen forward with the fields the reference's varlen C entry drops (paged_attn.cpp:423-433):
  * LSE out (fp32 [num_heads, total_q], unpadded as export.cpp:827; total_q = cu_seqlens_q[batch]
  * must be passed by the caller, it is only used to address the LSE), ALiBi, softcap,

@@ -1,0 +1,79 @@
+"""In-process A/B timing of kernel variants (interleaved rounds, one process, one device —
+cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/perf_ab.py --opt fwd_waves=4,8 [--mode fwd|bwd|fwdbwd] [--rounds 5]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--opt", action="append", default=[], help="name=v1,v2,...")
+    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwdbwd"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--b", type=int, default=4)
+    ap.add_argument("--h", type=int, default=32)
+    ap.add_argument("--hk", type=int, default=0)
+    ap.add_argument("--s", type=int, default=4096)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--dtype", default="bf16")
+    a = ap.parse_args()
+
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    variants = [[]]
+    for spec in a.opt:
+        name, vals = spec.split("=")
+        variants = [v + [(name, int(x))] for v in variants for x in vals.split(",")]
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+    hk = a.hk or a.h
+    causal = not a.noncausal
+    q = torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=dt)
+    k = torch.randn(a.b, a.s, hk, a.d, device="cuda", dtype=dt)
+    v = torch.randn(a.b, a.s, hk, a.d, device="cuda", dtype=dt)
+    do = torch.randn_like(q)
+    out = torch.empty_like(q)
+    pa = xfa.paged_attn
+    sc = a.d ** -0.5
+    lse = pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)[5]
+
+    def run():
+        if a.mode in ("fwd", "fwdbwd"):
+            pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)
+        if a.mode in ("bwd", "fwdbwd"):
+            pa.bwd(do, q, k, v, out, lse, None, None, None, None, 0.0, sc, causal, -1, -1, 0.0,
+                   False, None, None)
+
+    fl = 4.0 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0)
+    fl *= {"fwd": 1.0, "bwd": 2.5, "fwdbwd": 3.5}[a.mode]
+    res = {str(vv): [] for vv in variants}
+    for r in range(a.rounds):
+        for vv in variants:
+            for name, val in vv:
+                assert L.fmha_set_option(name.encode(), val) == 0, L.fmha_last_error()
+            run(); torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                run()
+            e.record(); torch.cuda.synchronize()
+            res[str(vv)].append(s.elapsed_time(e) / a.iters)
+    for vv, ts in res.items():
+        med = statistics.median(ts)
+        print(f"{a.mode} {vv}: median {med:.4f} ms  min {min(ts):.4f}  -> {fl / med / 1e9:.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -36,8 +36,10 @@ _SIGS = {
     "fmha_last_error": [],
     "fmha_last_status": [],
     "fmha_version": [],
+    "fmha_set_option": [C.c_char_p, C.c_int],
 }
 _RES = {"fmha_last_error": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
+        "fmha_set_option": C.c_int,
         "fmha_bwd_workspace_size": sz, "fmha_varlen_bwd_workspace_size": sz}
 
 EXPORTED = tuple(_SIGS)

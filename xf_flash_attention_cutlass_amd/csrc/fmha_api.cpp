@@ -26,6 +26,13 @@
 
 using namespace xfa;
 
+namespace xfa {
+Options& options() {
+    static Options o;
+    return o;
+}
+}  // namespace xfa
+
 namespace {
 
 thread_local std::string g_err;
@@ -174,6 +181,10 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         p.oaccum = (float*)base;
         p.lseaccum = (float*)(base + (size_t)splits * rows * hd * sizeof(float));
     }
+    p.prio_hi = options().fwd_prio;
+    p.sched_mode = options().fwd_sched;
+    p.store8 = options().fwd_store8;
+    options().num_cus = num_cus();
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
 
@@ -184,6 +195,23 @@ extern "C" {
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 const char* fmha_version(void) { return "xf-fmha-gfx950 1.0"; }
+
+int fmha_set_option(const char* name, int value) {
+    clear_error();
+    if (!name) { fail(1, "option name is null"); return -1; }
+    if (!strcmp(name, "fwd_waves")) {
+        if (value != 4 && value != 8) { fail(1, "fwd_waves must be 4 or 8"); return -1; }
+        options().fwd_waves = value;
+        return 0;
+    }
+    if (!strcmp(name, "fwd_prio")) { options().fwd_prio = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_pp")) { options().fwd_pp = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_sched")) { options().fwd_sched = value; return 0; }
+    if (!strcmp(name, "fwd_store8")) { options().fwd_store8 = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
+    fail(1, "unknown option '%s'", name);
+    return -1;
+}
 
 void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_slopes_ptr,
               const int32_t seqlen_q, const int32_t seqlen_k, const int32_t batch_size,

@@ -18,7 +18,19 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// Raw buffer access (SRD in SGPRs, 32-bit per-lane byte offset, hardware range check):
+// a load whose offset is past `bytes` returns zeros — used instead of `ok ? load : 0`
+// selects, which hipcc lowers to a branch + vmcnt(0) drain per load.
+constexpr int kOOB = 0x7FFFFF00;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+}
 
 constexpr int kBlockN = 64;   // keys per K/V tile (one LDS stage)
 constexpr float kLog2e = 1.4426950408889634f;
@@ -58,6 +70,11 @@ struct FwdParams {
     int num_splits;
     int kv_fp8;                // 1: K/V stored as fp8 e4m3fn
     float k_scale, v_scale;
+    int prio_hi;               // 1: waves NW/2.. run at s_setprio 1 (static, guide T5)
+    int sched_mode;            // bit0/bit1: pinned read-ahead interleave in PV / QK^T (pp)
+    int store8;                // 1: legacy 8-byte O stores (A/B knob for the 16-byte tail)
+    int persistent;            // 1: persistent grid walking (row block, b*hk) items
+    int n_mblocks;             // row blocks per (b, kv head) (persistent mode)
 };
 
 struct CombineParams {
@@ -151,6 +168,45 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 __device__ __forceinline__ float fast_tanh(float x) {
     const float e = __builtin_amdgcn_exp2f(x * (2.f * 1.4426950408889634f));
     return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+// Store one query row of the O^T accumulators (lane holds row lane&31, columns
+// 32dt + 8g + 4hh .. +3 in registers 4g..4g+3 of acc[dt]) as 16-byte stores: pairs of column
+// groups are exchanged between the lane halves with v_permlane32_swap so each lane writes 8
+// contiguous columns (8 x 16 B per lane instead of 16 x 8 B; the tail is store-issue-bound,
+// cdna_hip_programming.md T21).  Columns >= d (a multiple of 8) are not written.
+template <typename T, int ND>
+__device__ __forceinline__ void store_o_row16(T* orow, const f32x16 (&acc)[ND], float inv, int d, int hh) {
+    typedef __attribute__((ext_vector_type(2))) T T2;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+            const T2 a0v = {(T)(acc[dt][4 * gp] * inv), (T)(acc[dt][4 * gp + 1] * inv)};
+            const T2 a1v = {(T)(acc[dt][4 * gp + 2] * inv), (T)(acc[dt][4 * gp + 3] * inv)};
+            const T2 b0v = {(T)(acc[dt][4 * gp + 4] * inv), (T)(acc[dt][4 * gp + 5] * inv)};
+            const T2 b1v = {(T)(acc[dt][4 * gp + 6] * inv), (T)(acc[dt][4 * gp + 7] * inv)};
+            const auto r0 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a0v),
+                                                             __builtin_bit_cast(unsigned, b0v), false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a1v),
+                                                             __builtin_bit_cast(unsigned, b1v), false, false);
+            const int col = 32 * dt + 8 * gp + 8 * hh;
+            if (col < d) *reinterpret_cast<u32x4*>(orow + col) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+        }
+}
+
+template <typename T, int ND>
+__device__ __forceinline__ void store_o_row8(T* orow, const f32x16 (&acc)[ND], float inv, int d, int hh) {
+    typedef __attribute__((ext_vector_type(4))) T T4;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            if (32 * dt + 8 * g < d) {
+                const T4 v = {(T)(acc[dt][4 * g] * inv), (T)(acc[dt][4 * g + 1] * inv),
+                              (T)(acc[dt][4 * g + 2] * inv), (T)(acc[dt][4 * g + 3] * inv)};
+                *reinterpret_cast<T4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
+            }
 }
 
 // fp8 e4m3fn (OCP) -> f32, exact.

@@ -3,6 +3,7 @@
 // keeps the per-variant kernels in separate code objects (co-compiled template variants
 // perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
 #include "fmha_fwd_kernel.h"
+#include "fmha_fwd_pp_kernel.h"
 #include "fmha_launch.h"
 
 #ifndef XFA_HD
@@ -21,30 +22,52 @@ typedef __bf16 elem_t;
 typedef _Float16 elem_t;
 #endif
 
-template <int HD, typename T>
-static hipError_t launch_fwd_impl(const FwdParams& p, hipStream_t st) {
-    constexpr int NW = kFwdWaves;
+template <int HD, typename T, int NW, bool PP>
+static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     const bool mask = p.wl >= 0 || p.wr >= 0;
     const bool feat = p.alibi || p.softcap_pre > 0.f || p.cu_seqlens_q || p.cu_seqlens_k ||
                       p.seqused_k || p.block_table || p.num_splits > 1 || p.kv_fp8;
-    const dim3 grid(p.b * p.hk, fwd_num_m_blocks(p.seqlen_q, p.group), p.num_splits > 1 ? p.num_splits : 1);
-    const size_t smem = 2 * 2 * kBlockN * HD * 2;
-    void (*kern)(const FwdParams) =
-        mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
-             : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
+    const int rows = p.seqlen_q * p.group;
+    const int n_mb = (rows + NW * 32 - 1) / (NW * 32);
+    dim3 grid(p.b * p.hk, n_mb, p.num_splits > 1 ? p.num_splits : 1);
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    if (!PP && options().fwd_persistent > 0) {
+        const int items = p.b * p.hk * n_mb;
+        const int slots = options().num_cus * options().fwd_persistent;
+        if (items > slots) { pp.persistent = 1; grid = dim3(slots, 1, grid.z); }
+    }
+    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(2 * 2 * kBlockN * HD * 2);
+    void (*kern)(const FwdParams);
+    if constexpr (PP) {
+        const int sm = options().fwd_sched;
+        if (!feat && sm == 1) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 1> : fmha_fwd_pp_kernel<HD, T, false, false, 1>;
+        else if (!feat && sm == 2) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 2> : fmha_fwd_pp_kernel<HD, T, false, false, 2>;
+        else if (!feat && sm == 3) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 3> : fmha_fwd_pp_kernel<HD, T, false, false, 3>;
+        else kern = mask ? (feat ? fmha_fwd_pp_kernel<HD, T, true, true> : fmha_fwd_pp_kernel<HD, T, true, false>)
+                         : (feat ? fmha_fwd_pp_kernel<HD, T, false, true> : fmha_fwd_pp_kernel<HD, T, false, false>);
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    } else {
+        kern = mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
+                    : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
+    }
     static bool attr_done = false;   // benign race: idempotent attribute set
     if (!attr_done) {
-        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if constexpr (PP) {
+            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        } else {
+            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        }
         attr_done = true;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, p);
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
 
@@ -57,13 +80,15 @@ static hipError_t launch_fwd_impl(const FwdParams& p, hipStream_t st) {
     cp.lse_batch = p.lse_batch; cp.lse_head = p.lse_head;
     cp.b = p.b; cp.h = p.h; cp.seqlen_q = p.seqlen_q; cp.d = p.d; cp.hd = HD;
     cp.num_splits = p.num_splits;
-    const int64_t rows = (int64_t)p.b * p.h * p.seqlen_q;
-    hipLaunchKernelGGL((fmha_combine_kernel<HD, T>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, cp);
+    const int64_t crow = (int64_t)p.b * p.h * p.seqlen_q;
+    hipLaunchKernelGGL((fmha_combine_kernel<HD, T>), dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
     return hipGetLastError();
 }
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
-    return launch_fwd_impl<XFA_HD, elem_t>(p, st);
+    if (options().fwd_pp) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
+    if (options().fwd_waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8, false>(p, st);
+    return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
 }
 
 }  // namespace xfa

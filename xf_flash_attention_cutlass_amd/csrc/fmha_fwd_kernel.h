@@ -26,8 +26,10 @@
 
 namespace xfa {
 
+// One work item = (batch x kv-head, query row block, split).
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
-__global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p) {
+__device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const int bh,
+                                         const int m_block, const int split) {
     using V8 = typename DT<T>::v8;
     constexpr int NT = NW * 64;
     constexpr int BM = NW * 32;
@@ -38,19 +40,14 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     constexpr int ND = HD / 32;                 // 32-wide d tiles of O^T
     static_assert(NLD >= 1 && (NT % CPR) == 0, "tile/thread geometry");
 
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int lr = lane & 31;
     const int hh = lane >> 5;
 
-    const int bh = blockIdx.x;
     const int bidx = bh / p.hk;
     const int hk_i = bh - bidx * p.hk;
-    const int m_block = gridDim.y - 1 - blockIdx.y;   // heaviest (causal) row blocks first
-    const int split = blockIdx.z;
 
     int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
     if (FEAT) {
@@ -103,13 +100,15 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][16s + 8hh .. +7]
     V8 qf[NS];
     {
-        const T* qrow = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
-                        (int64_t)(q_off + pos) * p.q_row + (int64_t)head * p.q_head;
+        const T* qseq = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch + (int64_t)q_off * p.q_row;
+        const uint32_t qbytes = (uint32_t)(((int64_t)(sq - 1) * p.q_row + (int64_t)(p.h - 1) * p.q_head + p.d) * 2);
+        const __amdgpu_buffer_rsrc_t qr = make_rsrc(qseq, qbytes);
+        const int qrow_off = (int)(((int64_t)pos * p.q_row + (int64_t)head * p.q_head) * 2);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int d0 = 16 * s + 8 * hh;
-            if (row_ok && d0 < p.d) qf[s] = *reinterpret_cast<const V8*>(qrow + d0);
-            else qf[s] = V8{};
+            const int off = (row_ok && d0 < p.d) ? qrow_off + d0 * 2 : kOOB;
+            qf[s] = __builtin_bit_cast(V8, buf_load16(qr, off));
         }
     }
 
@@ -118,33 +117,40 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     const int lrow0 = tid / CPR;
     constexpr int LROW_STEP = NT / CPR;
     const bool lc_ok = lc * 8 < p.d;
-    const T* kbase = reinterpret_cast<const T*>(p.k) + (int64_t)hk_i * p.k_head + lc * 8;
-    const T* vbase = reinterpret_cast<const T*>(p.v) + (int64_t)hk_i * p.v_head + lc * 8;
     const bool paged = FEAT && p.block_table != nullptr;
-    if (!paged) {
-        kbase += (int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row;
-        vbase += (int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row;
-    }
+    // dense / varlen: one SRD per K and V covering this sequence's rows of this kv head
+    const T* kseq = reinterpret_cast<const T*>(p.k) + (int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row +
+                    (int64_t)hk_i * p.k_head;
+    const T* vseq = reinterpret_cast<const T*>(p.v) + (int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row +
+                    (int64_t)hk_i * p.v_head;
+    const uint32_t kbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.k_row + p.d) * 2);
+    const uint32_t vbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.v_row + p.d) * 2);
+    const __amdgpu_buffer_rsrc_t krs = make_rsrc(kseq, kbytes);
+    const __amdgpu_buffer_rsrc_t vrs = make_rsrc(vseq, vbytes);
+    // paged: per-row page pointers (clamped, unconditional loads + data select)
+    const T* kpool = reinterpret_cast<const T*>(p.k) + (int64_t)hk_i * p.k_head + lc * 8;
+    const T* vpool = reinterpret_cast<const T*>(p.v) + (int64_t)hk_i * p.v_head + lc * 8;
     const int* btab = paged ? p.block_table + (int64_t)bidx * p.bt_stride : nullptr;
 
-    uint4 kr[NLD], vr[NLD];
+    u32x4 kr[NLD], vr[NLD];
     auto load_tile = [&](int nb) {
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int n = nb * kBlockN + lrow0 + i * LROW_STEP;
             const bool ok = lc_ok && n < sk;
-            int64_t ko, vo;
             if (paged) {
-                const int pg = ok ? btab[n / p.page_size] : 0;
-                const int pr = n - (n / p.page_size) * p.page_size;
-                ko = (int64_t)pg * p.k_batch + (int64_t)pr * p.k_row;
-                vo = (int64_t)pg * p.v_batch + (int64_t)pr * p.v_row;
+                const int nc = ok ? n : 0;
+                const int pi = nc / p.page_size;
+                const int pg = btab[pi];
+                const int pr = nc - pi * p.page_size;
+                const u32x4 kx = *reinterpret_cast<const u32x4*>(kpool + (int64_t)pg * p.k_batch + (int64_t)pr * p.k_row);
+                const u32x4 vx = *reinterpret_cast<const u32x4*>(vpool + (int64_t)pg * p.v_batch + (int64_t)pr * p.v_row);
+                kr[i] = ok ? kx : u32x4{0, 0, 0, 0};
+                vr[i] = ok ? vx : u32x4{0, 0, 0, 0};
             } else {
-                ko = (int64_t)n * p.k_row;
-                vo = (int64_t)n * p.v_row;
+                kr[i] = buf_load16(krs, ok ? n * (int)p.k_row * 2 + lc * 16 : kOOB);
+                vr[i] = buf_load16(vrs, ok ? n * (int)p.v_row * 2 + lc * 16 : kOOB);
             }
-            kr[i] = ok ? *reinterpret_cast<const uint4*>(kbase + ko) : make_uint4(0, 0, 0, 0);
-            vr[i] = ok ? *reinterpret_cast<const uint4*>(vbase + vo) : make_uint4(0, 0, 0, 0);
         }
     };
     auto store_tile = [&](int buf) {
@@ -152,8 +158,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int r = lrow0 + i * LROW_STEP;
-            *reinterpret_cast<uint4*>(ks + lds_off<HD>(r, lc)) = kr[i];
-            *reinterpret_cast<uint4*>(ks + TILE + lds_off<HD>(r, lc)) = vr[i];
+            *reinterpret_cast<u32x4*>(ks + lds_off<HD>(r, lc)) = kr[i];
+            *reinterpret_cast<u32x4*>(ks + TILE + lds_off<HD>(r, lc)) = vr[i];
         }
     };
 
@@ -182,8 +188,13 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     if (nb_lo < nb_hi) {
         load_tile(nb_lo);
         store_tile(0);
-        __syncthreads();
     }
+    // Retire every prologue load (the Q fragments) here: otherwise the loop-header merge of
+    // the waitcnt scoreboard makes the first QK^T MFMA of EVERY iteration wait vmcnt(0), i.e.
+    // drain the next tile's prefetch (vmcnt=0, expcnt=7, lgkmcnt=15).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    if (p.prio_hi && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     int buf = 0;
     for (int nb = nb_lo; nb < nb_hi; ++nb) {
         const bool more = nb + 1 < nb_hi;
@@ -238,22 +249,27 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
             mx = wave_max_halves(mx);
             const float m_new = fmaxf(m_run, mx);
             const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
-            const float alpha = fast_exp2(m_run * c - mref);
-            m_run = m_new;
-            float rs = 0.f;
+            // Exact lazy rescale: only when some row of this wave raised its running max
+            // (the O^T rescale is a 64-register VALU pass; after the first tiles it is rare).
+            if (__any(m_new > m_run)) {
+                const float alpha = fast_exp2(m_run * c - mref);
+                l_run *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+                m_run = m_new;
+            }
+            float rs[4] = {0.f, 0.f, 0.f, 0.f};   // 4 independent chains, not one 32-long
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float e = fast_exp2(fmaf(st[kt][r], c, -mref));
                     st[kt][r] = e;
-                    rs += e;
+                    rs[r & 3] += e;
                 }
-            l_run = fmaf(l_run, alpha, rs);
-#pragma unroll
-            for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+            l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
             // ---- O^T += V^T P^T : P accumulator registers are the B operand as they stand
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
@@ -302,21 +318,37 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     }
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
               (int64_t)(q_off + pos) * p.o_row + (int64_t)head * p.o_head;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int d = 32 * dt + 8 * g + 4 * hh;
-            if (d < p.d) {
-                typedef __attribute__((ext_vector_type(4))) T T4;
-                T4 v = {(T)(acc_o[dt][4 * g] * inv), (T)(acc_o[dt][4 * g + 1] * inv),
-                        (T)(acc_o[dt][4 * g + 2] * inv), (T)(acc_o[dt][4 * g + 3] * inv)};
-                *reinterpret_cast<T4*>(orow + d) = v;
-            }
-        }
+    if (p.store8) store_o_row8<T, ND>(orow, acc_o, inv, p.d, hh);
+    else store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
     if (p.lse && hh == 0) {
         p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] =
             empty ? INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+    }
+}
+
+// Grid: either one workgroup per item (grid = (b*hk, m_blocks, splits), heaviest causal row
+// blocks dispatched first), or persistent (p.persistent: grid = (resident workgroups, 1,
+// splits)), each workgroup walking items in a heaviest-first boustrophedon order so the
+// causal work per workgroup balances, and one item's O-store tail overlaps the next item's
+// prologue loads instead of a workgroup boundary.
+template <int HD, typename T, int NW, bool MASK, bool FEAT>
+__global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nbh = p.b * p.hk;
+    const int g = gridDim.x;
+    for (int k = 0;; ++k) {        // one call site: the item body is inlined once
+        int bh, m_block;
+        if (p.persistent) {
+            const int lin = k * g + ((k & 1) ? g - 1 - (int)blockIdx.x : (int)blockIdx.x);
+            if (lin >= nbh * p.n_mblocks) break;
+            bh = lin % nbh;
+            m_block = p.n_mblocks - 1 - lin / nbh;
+        } else {
+            if (k > 0) break;
+            bh = blockIdx.x;
+            m_block = gridDim.y - 1 - blockIdx.y;
+        }
+        fwd_item<HD, T, NW, MASK, FEAT>(p, smem, bh, m_block, blockIdx.z);
     }
 }
 

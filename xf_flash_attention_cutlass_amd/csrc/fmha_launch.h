@@ -8,8 +8,17 @@
 
 namespace xfa {
 
-constexpr int kFwdWaves = 4;                 // waves per forward workgroup
-constexpr int kFwdBlockM = kFwdWaves * 32;   // query rows per forward workgroup
+// Tuning knobs, settable through fmha_set_option() (used for in-process A/B runs).
+struct Options {
+    int fwd_waves = 8;        // waves per forward workgroup (4 or 8); 32 query rows per wave
+    int fwd_prio = 0;         // static s_setprio 1 for the younger half of the workgroup
+    int fwd_pp = 0;           // 1: ping-pong forward schedule (8 waves, fmha_fwd_pp_kernel.h)
+    int fwd_sched = 0;        // sched_group_barrier interleave bits (experiment knob)
+    int fwd_store8 = 0;       // legacy 8-byte O stores (A/B knob)
+    int fwd_persistent = 1;   // persistent grid (workgroups per CU; 0 = one workgroup per item)
+    int num_cus = 256;        // filled by the C ABI from the device
+};
+Options& options();
 
 // Forward for head dim bucket HD (64 or 128) and dtype; launches the combine when
 // p.num_splits > 1.  Returns the launch status.
@@ -24,8 +33,9 @@ hipError_t launch_bwd_hd64_f16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_bf16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_f16(const BwdParams& p, hipStream_t st);
 
+inline int fwd_block_m() { return options().fwd_pp ? 256 : options().fwd_waves * 32; }
 inline int fwd_num_m_blocks(int seqlen_q, int group) {
-    return (seqlen_q * group + kFwdBlockM - 1) / kFwdBlockM;
+    return (seqlen_q * group + fwd_block_m() - 1) / fwd_block_m();
 }
 
 }  // namespace xfa
