@@ -250,3 +250,75 @@ def test_paged_indexing_bitexact(xfa, num_splits, sq, hk):
     r, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm)
     pt, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm, upcast=False, reorder_ops=True)
     _assert_parity(paged, r, pt, mult=3.0, atol=1e-5, what="paged")
+
+
+def _fp8_cache(x, scale, dt=torch.bfloat16):
+    """Quantise a cache to OCP e4m3fn with a per-tensor scale; returns (fp8, dequant-as-dt)
+    where dequant = dt(f32(fp8) * scale), the kernel's own conversion."""
+    q8 = (x.float() / scale).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q8, (q8.float() * scale).to(dt)
+
+
+@pytest.mark.parametrize("num_splits", [1, 0, 3])
+@pytest.mark.parametrize("sq,hk", [(1, 8), (1, 2), (4, 2)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
+def test_paged_fp8_cache(xfa, num_splits, sq, hk, dtype):
+    """fp8 (e4m3fn) paged cache == the bf16/fp16 path over the dequantised cache, bit for bit;
+    and within the kvcache tolerance of the oracle.  (No reference counterpart: the reference
+    has no fp8 cache — SURVEY §8d C5 is this build's extension, parity pinned by the
+    dequantised-cache equality, not by a reference fixture.)"""
+    torch.manual_seed(1)
+    dt = _dtype(dtype)
+    b, h, d, page, sk = 3, 8, 128, 16, 1000
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    ks, vs = 0.0123, 0.0371  # not powers of two: the dequant rounding is exercised
+    kp8, kpd = _fp8_cache(kp, ks, dt)
+    vp8, vpd = _fp8_cache(vp, vs, dt)
+    q = torch.randn(b, sq, h, d).to(dt).to(DEV)
+    seqlens = torch.tensor([1000, 517, 33], dtype=torch.int32).to(DEV)
+    tab = table.to(DEV)
+    out8, lse8 = xfa.flash_attn_with_kvcache(q, kp8.to(DEV), vp8.to(DEV), cache_seqlens=seqlens,
+                                             block_table=tab, num_splits=num_splits,
+                                             return_softmax_lse=True, k_scale=ks, v_scale=vs)
+    outd, lsed = xfa.flash_attn_with_kvcache(q, kpd.to(DEV), vpd.to(DEV), cache_seqlens=seqlens,
+                                             block_table=tab, num_splits=num_splits,
+                                             return_softmax_lse=True)
+    assert torch.equal(out8, outd)
+    assert torch.equal(lse8, lsed)
+    nblk = table.shape[1]
+    kfull = kpd[table.long().flatten()].reshape(b, nblk * page, hk, d)[:, :sk]
+    vfull = vpd[table.long().flatten()].reshape(b, nblk * page, hk, d)[:, :sk]
+    kpm = torch.arange(sk).view(1, -1) < seqlens.cpu().view(-1, 1)
+    r, _ = orc.attention_ref(q.cpu(), kfull, vfull, None, kpm)
+    pt, _ = orc.attention_ref(q.cpu(), kfull, vfull, None, kpm, upcast=False, reorder_ops=True)
+    _assert_parity(out8, r, pt, mult=3.0, atol=1e-5, what="paged fp8")
+
+
+def test_paged_fp8_capi(xfa):
+    """fmha_page_kvcache_fwd_ex(kv_dtype=1) through the C ABI == the pybind fp8 op, bitwise;
+    an unknown kv_dtype is rejected."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(2)
+    b, h, hk, d, page, sk = 2, 8, 2, 128, 16, 256
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    kp8, _ = _fp8_cache(kp, 0.02)
+    vp8, _ = _fp8_cache(vp, 0.03)
+    q = torch.randn(b, 1, h, d).bfloat16().to(DEV)
+    seqlens = torch.tensor([256, 100], dtype=torch.int32).to(DEV)
+    tab, k8, v8 = table.to(DEV), kp8.to(DEV), vp8.to(DEV)
+    ref = xfa.flash_attn_with_kvcache(q, k8, v8, cache_seqlens=seqlens, block_table=tab,
+                                      k_scale=0.02, v_scale=0.03, num_splits=1)
+    out = torch.empty_like(q)
+    lse = torch.empty(b, h, 1, device=DEV, dtype=torch.float32)
+    args = [q.data_ptr(), k8.data_ptr(), v8.data_ptr(), out.data_ptr(), lse.data_ptr(),
+            tab.data_ptr(), tab.stride(0), seqlens.data_ptr(), 1, sk, b, h, hk, d, page,
+            d ** -0.5, -1, -1, 0.0, None, 0, 1]
+    st = capi.stream_handle()
+    L.fmha_page_kvcache_fwd_ex(*args, 1, 0.02, 0.03, 0, st)
+    torch.cuda.synchronize()
+    assert L.fmha_last_status() == 0, L.fmha_last_error()
+    assert torch.equal(out, ref)
+    L.fmha_page_kvcache_fwd_ex(*args, 7, 1.0, 1.0, 0, st)
+    assert L.fmha_last_status() != 0
+    assert b"kv_dtype" in L.fmha_last_error()

@@ -324,7 +324,7 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
         REQUIRE(block_table, "block_table must be given for the paged KV path");
         REQUIRE(page_block_size > 0, "page_block_size must be positive");
         REQUIRE(seqlen_q > 0 && max_seqlen_k > 0, "seqlen_q / seqlen_k must be positive");
-        REQUIRE(kv_dtype == 0, "fp8 KV cache is not supported by this build yet");
+        REQUIRE(kv_dtype == 0 || kv_dtype == 1, "kv_dtype must be 0 (same as q) or 1 (fp8 e4m3fn)");
         FwdParams p{};
         const int h = num_heads, hk = num_heads_k, d = head_size;
         p.q = q; p.k = kcache; p.v = vcache; p.o = o; p.lse = (float*)softmax_lse;

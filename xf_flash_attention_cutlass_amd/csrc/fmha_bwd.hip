@@ -34,10 +34,10 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
     const size_t smem = 2 * (size_t)kBwdBlockN * HD * 2 + 2 * (size_t)kBwdBlockM * HD * 2 + kBwdBlockN * 64;
     static bool attr_done = false;
     if (!attr_done) {
-        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         attr_done = true;
     }
     const dim3 grid(p.b * p.hk, (p.seqlen_k + kBwdBlockN - 1) / kBwdBlockN);

@@ -31,6 +31,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
 }
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+__device__ __forceinline__ u32x2 buf_load8(__amdgpu_buffer_rsrc_t r, int voff) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+}
 
 constexpr int kBlockN = 64;   // keys per K/V tile (one LDS stage)
 constexpr float kLog2e = 1.4426950408889634f;
@@ -207,6 +211,19 @@ __device__ __forceinline__ void store_o_row8(T* orow, const f32x16 (&acc)[ND], f
                               (T)(acc[dt][4 * g + 2] * inv), (T)(acc[dt][4 * g + 3] * inv)};
                 *reinterpret_cast<T4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
             }
+}
+
+// 8 OCP fp8 e4m3fn values (two dwords) -> 8 x T = T(f32(fp8) * scale), packed in 4 dwords.
+template <typename T>
+__device__ __forceinline__ u32x4 fp8x8_to(unsigned lo, unsigned hi, float scale) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) T T2;
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8(lo, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(lo, true);
+    const f2 c = __builtin_amdgcn_cvt_pk_f32_fp8(hi, false), d = __builtin_amdgcn_cvt_pk_f32_fp8(hi, true);
+    const T2 ta = {(T)(a[0] * scale), (T)(a[1] * scale)}, tb = {(T)(b[0] * scale), (T)(b[1] * scale)};
+    const T2 tc = {(T)(c[0] * scale), (T)(c[1] * scale)}, td = {(T)(d[0] * scale), (T)(d[1] * scale)};
+    return u32x4{__builtin_bit_cast(unsigned, ta), __builtin_bit_cast(unsigned, tb),
+                 __builtin_bit_cast(unsigned, tc), __builtin_bit_cast(unsigned, td)};
 }
 
 // fp8 e4m3fn (OCP) -> f32, exact.

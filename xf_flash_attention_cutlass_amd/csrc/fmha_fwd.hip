@@ -47,7 +47,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         else if (!feat && sm == 3) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 3> : fmha_fwd_pp_kernel<HD, T, false, false, 3>;
         else kern = mask ? (feat ? fmha_fwd_pp_kernel<HD, T, true, true> : fmha_fwd_pp_kernel<HD, T, true, false>)
                          : (feat ? fmha_fwd_pp_kernel<HD, T, false, true> : fmha_fwd_pp_kernel<HD, T, false, false>);
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     } else {
         kern = mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
                     : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
@@ -55,15 +55,15 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     static bool attr_done = false;   // benign race: idempotent attribute set
     if (!attr_done) {
         if constexpr (PP) {
-            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         } else {
-            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         }
         attr_done = true;
     }
@@ -86,7 +86,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 }
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
-    if (options().fwd_pp) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
+    if (options().fwd_pp && !p.kv_fp8) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
     if (options().fwd_waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8, false>(p, st);
     return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
 }

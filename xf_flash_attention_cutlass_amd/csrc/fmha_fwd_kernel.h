@@ -118,18 +118,22 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     constexpr int LROW_STEP = NT / CPR;
     const bool lc_ok = lc * 8 < p.d;
     const bool paged = FEAT && p.block_table != nullptr;
+    // fp8 (OCP e4m3fn) K/V: 1-byte elements, dequantised to T with the per-tensor scale while
+    // staging (the LDS image and everything after it are unchanged)
+    const bool kv8 = FEAT && p.kv_fp8;
+    const int esz = kv8 ? 1 : 2;
     // dense / varlen: one SRD per K and V covering this sequence's rows of this kv head
-    const T* kseq = reinterpret_cast<const T*>(p.k) + (int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row +
-                    (int64_t)hk_i * p.k_head;
-    const T* vseq = reinterpret_cast<const T*>(p.v) + (int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row +
-                    (int64_t)hk_i * p.v_head;
-    const uint32_t kbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.k_row + p.d) * 2);
-    const uint32_t vbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.v_row + p.d) * 2);
+    const char* kseq = reinterpret_cast<const char*>(p.k) +
+                       ((int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row + (int64_t)hk_i * p.k_head) * esz;
+    const char* vseq = reinterpret_cast<const char*>(p.v) +
+                       ((int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row + (int64_t)hk_i * p.v_head) * esz;
+    const uint32_t kbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.k_row + p.d) * esz);
+    const uint32_t vbytes = (uint32_t)(((int64_t)(sk > 0 ? sk - 1 : 0) * p.v_row + p.d) * esz);
     const __amdgpu_buffer_rsrc_t krs = make_rsrc(kseq, kbytes);
     const __amdgpu_buffer_rsrc_t vrs = make_rsrc(vseq, vbytes);
     // paged: per-row page pointers (clamped, unconditional loads + data select)
-    const T* kpool = reinterpret_cast<const T*>(p.k) + (int64_t)hk_i * p.k_head + lc * 8;
-    const T* vpool = reinterpret_cast<const T*>(p.v) + (int64_t)hk_i * p.v_head + lc * 8;
+    const char* kpool = reinterpret_cast<const char*>(p.k) + ((int64_t)hk_i * p.k_head + lc * 8) * esz;
+    const char* vpool = reinterpret_cast<const char*>(p.v) + ((int64_t)hk_i * p.v_head + lc * 8) * esz;
     const int* btab = paged ? p.block_table + (int64_t)bidx * p.bt_stride : nullptr;
 
     u32x4 kr[NLD], vr[NLD];
@@ -143,10 +147,24 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 const int pi = nc / p.page_size;
                 const int pg = btab[pi];
                 const int pr = nc - pi * p.page_size;
-                const u32x4 kx = *reinterpret_cast<const u32x4*>(kpool + (int64_t)pg * p.k_batch + (int64_t)pr * p.k_row);
-                const u32x4 vx = *reinterpret_cast<const u32x4*>(vpool + (int64_t)pg * p.v_batch + (int64_t)pr * p.v_row);
-                kr[i] = ok ? kx : u32x4{0, 0, 0, 0};
-                vr[i] = ok ? vx : u32x4{0, 0, 0, 0};
+                const char* ka = kpool + ((int64_t)pg * p.k_batch + (int64_t)pr * p.k_row) * esz;
+                const char* va = vpool + ((int64_t)pg * p.v_batch + (int64_t)pr * p.v_row) * esz;
+                if (kv8) {
+                    const uint2 kx = *reinterpret_cast<const uint2*>(ka);
+                    const uint2 vx = *reinterpret_cast<const uint2*>(va);
+                    kr[i] = ok ? fp8x8_to<T>(kx.x, kx.y, p.k_scale) : u32x4{0, 0, 0, 0};
+                    vr[i] = ok ? fp8x8_to<T>(vx.x, vx.y, p.v_scale) : u32x4{0, 0, 0, 0};
+                } else {
+                    const u32x4 kx = *reinterpret_cast<const u32x4*>(ka);
+                    const u32x4 vx = *reinterpret_cast<const u32x4*>(va);
+                    kr[i] = ok ? kx : u32x4{0, 0, 0, 0};
+                    vr[i] = ok ? vx : u32x4{0, 0, 0, 0};
+                }
+            } else if (kv8) {
+                const u32x2 kx = buf_load8(krs, ok ? n * (int)p.k_row + lc * 8 : kOOB);
+                const u32x2 vx = buf_load8(vrs, ok ? n * (int)p.v_row + lc * 8 : kOOB);
+                kr[i] = fp8x8_to<T>(kx[0], kx[1], p.k_scale);
+                vr[i] = fp8x8_to<T>(vx[0], vx[1], p.v_scale);
             } else {
                 kr[i] = buf_load16(krs, ok ? n * (int)p.k_row * 2 + lc * 16 : kOOB);
                 vr[i] = buf_load16(vrs, ok ? n * (int)p.v_row * 2 + lc * 16 : kOOB);

@@ -475,6 +475,46 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     return {dq, dk, dv, softmax_d};
 }
 
+// Paged decode over an fp8 (OCP e4m3fn) K/V cache with per-tensor dequant scales — an
+// extension the reference lacks.  kcache/vcache: float8_e4m3fn (or uint8 bytes)
+// [num_blocks, page, hk, d]; returns {out, softmax_lse}.
+std::vector<at::Tensor>
+mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcache,
+                    const at::Tensor& seqlens_k, const at::Tensor& block_table, const float k_scale,
+                    const float v_scale, const float softmax_scale, bool is_causal,
+                    int window_size_left, int window_size_right, int num_splits) {
+    auto dt = q.dtype();
+    TORCH_CHECK(dt == torch::kFloat16 || dt == torch::kBFloat16, "q must be fp16 or bf16");
+    TORCH_CHECK(kcache.element_size() == 1 && vcache.element_size() == 1, "fp8 K/V cache expected");
+    CHECK_DEVICE(q); CHECK_DEVICE(kcache); CHECK_DEVICE(vcache); CHECK_DEVICE(block_table); CHECK_DEVICE(seqlens_k);
+    CHECK_CONTIGUOUS(kcache); CHECK_CONTIGUOUS(vcache);
+    TORCH_CHECK(block_table.dtype() == torch::kInt32 && seqlens_k.dtype() == torch::kInt32,
+                "block_table / seqlens_k must be int32");
+    const int batch_size = q.size(0), seqlen_q = q.size(1), num_heads = q.size(2), d = q.size(3);
+    const int page = kcache.size(1), num_heads_k = kcache.size(2);
+    TORCH_CHECK(kcache.size(3) == d && d % 8 == 0 && d <= 128, "head_size must be a multiple of 8 and <= 128");
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    CHECK_SHAPE(block_table, batch_size, block_table.size(1));
+    CHECK_SHAPE(seqlens_k, batch_size);
+    const int seqlen_k = block_table.size(1) * page;
+    if (seqlen_q == 1) is_causal = false;
+    if (is_causal) window_size_right = 0;
+    if (window_size_left >= seqlen_k) window_size_left = -1;
+    if (window_size_right >= seqlen_k) window_size_right = -1;
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    auto qc = q.contiguous();
+    auto out = torch::empty_like(qc);
+    auto lse = torch::empty({batch_size, num_heads, seqlen_q}, q.options().dtype(at::kFloat));
+    auto bt = block_table.contiguous();
+    fmha_page_kvcache_fwd_ex(qc.data_ptr(), kcache.data_ptr(), vcache.data_ptr(), out.data_ptr(),
+                             lse.data_ptr(), bt.data_ptr(), (int)bt.stride(0), seqlens_k.data_ptr(),
+                             seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, d, page,
+                             softmax_scale, window_size_left, window_size_right, 0.f, nullptr, 0,
+                             num_splits, 1, k_scale, v_scale, dt == torch::kFloat16, cur_stream());
+    raise_if_failed("fwd_kvcache_fp8");
+    return {out, lse};
+}
+
 PYBIND11_MODULE(paged_attn, m) {
     m.doc() = "FlashAttention for MI355X (gfx950): hand-written HIP kernels behind the paged_attn C ABI";
     m.def("fwd", &mha_fwd, "Forward pass");
@@ -482,5 +522,6 @@ PYBIND11_MODULE(paged_attn, m) {
     m.def("fwd_kvcache", &mha_fwd_kvcache, "Forward pass, with KV-cache");
     m.def("bwd", &mha_bwd, "Backward pass");
     m.def("varlen_bwd", &mha_varlen_bwd, "Backward pass (variable length)");
+    m.def("fwd_kvcache_fp8", &mha_fwd_kvcache_fp8, "Paged decode over an fp8 e4m3fn K/V cache");
     m.def("version", []() { return std::string(fmha_version()); });
 }

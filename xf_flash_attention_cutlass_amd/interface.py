@@ -126,8 +126,11 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
                             block_table: Optional[torch.Tensor] = None, softmax_scale=None,
                             causal=False, window_size=(-1, -1), softcap=0.0,
                             rotary_interleaved=True, alibi_slopes=None, num_splits=0,
-                            return_softmax_lse=False):
-    """Decode / chunked prefill against a (paged) KV cache (test.py:189-245)."""
+                            return_softmax_lse=False, k_scale=1.0, v_scale=1.0):
+    """Decode / chunked prefill against a (paged) KV cache (test.py:189-245).
+
+    Extension: a `torch.float8_e4m3fn` paged cache is read natively (dequantised in-kernel as
+    fp8 * k_scale / v_scale); it requires `block_table` and `cache_seqlens`."""
     assert k_cache.stride(-1) == 1, "k_cache must have contiguous last dimension"
     assert v_cache.stride(-1) == 1, "v_cache must have contiguous last dimension"
     if cache_leftpad is not None:
@@ -136,6 +139,20 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
     q, k, v = (_maybe_contiguous(x) for x in (q, k, v))
     if softmax_scale is None:
         softmax_scale = q.shape[-1] ** (-0.5)
+    if k_cache.dtype == torch.float8_e4m3fn:
+        if block_table is None or cache_seqlens is None or k is not None or alibi_slopes is not None \
+                or softcap > 0:
+            raise NotImplementedError("fp8 K/V cache: paged decode with block_table and "
+                                      "cache_seqlens only")
+        if isinstance(cache_seqlens, int):
+            cache_seqlens = torch.full((q.shape[0],), cache_seqlens, dtype=torch.int32,
+                                       device=q.device)
+        out, lse = paged_attn.fwd_kvcache_fp8(q, k_cache.view(torch.uint8),
+                                              v_cache.view(torch.uint8), cache_seqlens,
+                                              block_table, float(k_scale), float(v_scale),
+                                              softmax_scale, causal, int(window_size[0]),
+                                              int(window_size[1]), num_splits)
+        return (out, lse) if return_softmax_lse else out
     if cache_seqlens is not None and isinstance(cache_seqlens, int):
         cache_seqlens = torch.full((k_cache.shape[0],), cache_seqlens, dtype=torch.int32,
                                    device=k_cache.device)
