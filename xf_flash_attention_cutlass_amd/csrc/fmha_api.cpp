@@ -184,6 +184,8 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.prio_hi = options().fwd_prio;
     p.sched_mode = options().fwd_sched;
     p.store8 = options().fwd_store8;
+    p.pipe = options().fwd_pipe;
+    p.dbg = options().fwd_dbg;
     options().num_cus = num_cus();
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
@@ -209,6 +211,8 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_sched")) { options().fwd_sched = value; return 0; }
     if (!strcmp(name, "fwd_store8")) { options().fwd_store8 = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
+    if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     fail(1, "unknown option '%s'", name);
     return -1;
 }

@@ -79,6 +79,8 @@ struct FwdParams {
     int store8;                // 1: legacy 8-byte O stores (A/B knob for the 16-byte tail)
     int persistent;            // 1: persistent grid walking (row block, b*hk) items
     int n_mblocks;             // row blocks per (b, kv head) (persistent mode)
+    int pipe;                  // 1: software-pipelined loop over the unmasked key tiles
+    int dbg;                   // timing experiments only (results invalid when set)
 };
 
 struct CombineParams {
@@ -133,11 +135,20 @@ template <> struct DT<__bf16> {
     static __device__ __forceinline__ f32x16 mfma32(const v8& a, const v8& b, const f32x16& c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
     }
+    typedef __attribute__((ext_vector_type(2))) __bf16 v2;
+    // acc + a.x + a.y (v_dot2c_f32_bf16 against ones)
+    static __device__ __forceinline__ float sum2(const v2& a, float acc) {
+        return __builtin_amdgcn_fdot2_f32_bf16(a, v2{(__bf16)1.f, (__bf16)1.f}, acc, false);
+    }
 };
 template <> struct DT<_Float16> {
     typedef f16x8 v8;
     static __device__ __forceinline__ f32x16 mfma32(const v8& a, const v8& b, const f32x16& c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    typedef __attribute__((ext_vector_type(2))) _Float16 v2;
+    static __device__ __forceinline__ float sum2(const v2& a, float acc) {
+        return __builtin_amdgcn_fdot2(a, v2{(_Float16)1.f, (_Float16)1.f}, acc, false);
     }
 };
 

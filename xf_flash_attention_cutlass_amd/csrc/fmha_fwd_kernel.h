@@ -24,7 +24,14 @@
 
 #include "fmha_common.h"
 
+#include <type_traits>
+
 namespace xfa {
+
+#ifndef XFA_SCHED_FENCE
+#define XFA_SCHED_FENCE 1
+#endif
+constexpr bool SCHED_FENCE = XFA_SCHED_FENCE;
 
 // One work item = (batch x kv-head, query row block, split).
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
@@ -36,6 +43,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     constexpr int CPR = HD / 8;                 // 16-byte chunks per K/V row
     constexpr int NLD = kBlockN * CPR / NT;     // chunks per thread per tile
     constexpr int TILE = kBlockN * HD * 2;      // bytes of one K (or V) tile
+    constexpr int VREG = 3 * TILE;              // LDS: K tiles of buffers 0..2, then V tiles
     constexpr int NS = HD / 16;                 // k-steps of the QK^T product
     constexpr int ND = HD / 32;                 // 32-wide d tiles of O^T
     static_assert(NLD >= 1 && (NT % CPR) == 0, "tile/thread geometry");
@@ -137,7 +145,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     const int* btab = paged ? p.block_table + (int64_t)bidx * p.bt_stride : nullptr;
 
     u32x4 kr[NLD], vr[NLD];
-    auto load_tile = [&](int nb) {
+    auto load_to = [&](int nb, u32x4 (&ko)[NLD], u32x4 (&vo)[NLD]) {
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int n = nb * kBlockN + lrow0 + i * LROW_STEP;
@@ -152,39 +160,40 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 if (kv8) {
                     const uint2 kx = *reinterpret_cast<const uint2*>(ka);
                     const uint2 vx = *reinterpret_cast<const uint2*>(va);
-                    kr[i] = ok ? fp8x8_to<T>(kx.x, kx.y, p.k_scale) : u32x4{0, 0, 0, 0};
-                    vr[i] = ok ? fp8x8_to<T>(vx.x, vx.y, p.v_scale) : u32x4{0, 0, 0, 0};
+                    ko[i] = ok ? fp8x8_to<T>(kx.x, kx.y, p.k_scale) : u32x4{0, 0, 0, 0};
+                    vo[i] = ok ? fp8x8_to<T>(vx.x, vx.y, p.v_scale) : u32x4{0, 0, 0, 0};
                 } else {
                     const u32x4 kx = *reinterpret_cast<const u32x4*>(ka);
                     const u32x4 vx = *reinterpret_cast<const u32x4*>(va);
-                    kr[i] = ok ? kx : u32x4{0, 0, 0, 0};
-                    vr[i] = ok ? vx : u32x4{0, 0, 0, 0};
+                    ko[i] = ok ? kx : u32x4{0, 0, 0, 0};
+                    vo[i] = ok ? vx : u32x4{0, 0, 0, 0};
                 }
             } else if (kv8) {
                 const u32x2 kx = buf_load8(krs, ok ? n * (int)p.k_row + lc * 8 : kOOB);
                 const u32x2 vx = buf_load8(vrs, ok ? n * (int)p.v_row + lc * 8 : kOOB);
-                kr[i] = fp8x8_to<T>(kx[0], kx[1], p.k_scale);
-                vr[i] = fp8x8_to<T>(vx[0], vx[1], p.v_scale);
+                ko[i] = fp8x8_to<T>(kx[0], kx[1], p.k_scale);
+                vo[i] = fp8x8_to<T>(vx[0], vx[1], p.v_scale);
             } else {
-                kr[i] = buf_load16(krs, ok ? n * (int)p.k_row * 2 + lc * 16 : kOOB);
-                vr[i] = buf_load16(vrs, ok ? n * (int)p.v_row * 2 + lc * 16 : kOOB);
+                ko[i] = buf_load16(krs, ok ? n * (int)p.k_row * 2 + lc * 16 : kOOB);
+                vo[i] = buf_load16(vrs, ok ? n * (int)p.v_row * 2 + lc * 16 : kOOB);
             }
         }
     };
-    auto store_tile = [&](int buf) {
-        char* ks = smem + buf * 2 * TILE;
+    auto store_from = [&](int buf, const u32x4 (&ki)[NLD], const u32x4 (&vi)[NLD]) {
+        char* ks = smem + buf * TILE;
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int r = lrow0 + i * LROW_STEP;
-            *reinterpret_cast<u32x4*>(ks + lds_off<HD>(r, lc)) = kr[i];
-            *reinterpret_cast<u32x4*>(ks + TILE + lds_off<HD>(r, lc)) = vr[i];
+            *reinterpret_cast<u32x4*>(ks + lds_off<HD>(r, lc)) = ki[i];
+            *reinterpret_cast<u32x4*>(ks + VREG + lds_off<HD>(r, lc)) = vi[i];
         }
     };
 
-    // Per-lane LDS read offsets (row-independent parts of the swizzle).
-    int koff[NS];
+    // Per-lane LDS read addresses (row-independent parts of the swizzle); the
+    // buffer / half / row-block parts are compile-time offsets folded into the ds_read.
+    const char* kaddr[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) koff[s] = lds_off<HD>(lr, 2 * s + hh);
+    for (int s = 0; s < NS; ++s) kaddr[s] = smem + lds_off<HD>(lr, 2 * s + hh);
     const int q4 = (lane & 15) >> 2;
     int voff[2][ND];
 #pragma unroll
@@ -193,7 +202,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         for (int dt = 0; dt < ND; ++dt) {
             const int r = 4 * hh + q4 + 8 * part;
             const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            voff[part][dt] = VREG + lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
         }
     }
 
@@ -203,115 +212,247 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     float m_run = -INFINITY;
     float l_run = 0.f;
 
-    if (nb_lo < nb_hi) {
-        load_tile(nb_lo);
-        store_tile(0);
-    }
-    // Retire every prologue load (the Q fragments) here: otherwise the loop-header merge of
-    // the waitcnt scoreboard makes the first QK^T MFMA of EVERY iteration wait vmcnt(0), i.e.
-    // drain the next tile's prefetch (vmcnt=0, expcnt=7, lgkmcnt=15).
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-    if (p.prio_hi && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    int buf = 0;
-    for (int nb = nb_lo; nb < nb_hi; ++nb) {
-        const bool more = nb + 1 < nb_hi;
-        if (more) load_tile(nb + 1);
-        const char* ks = smem + buf * 2 * TILE;
-        const char* vs = ks + TILE;
-        const int n0 = nb * kBlockN;
-        const bool active = wave_ok && n0 < w_lr_max && n0 + kBlockN > w_ll_min;
-        if (active) {
-            // ---- S^T = K Q^T : two 32-key tiles
-            f32x16 st[2] = {f32x16{}, f32x16{}};
+    // ---- the pieces of one 64-key tile
+    // K operand of S^T = K Q^T for k-step s, 32-key half `kt`, read row-wise from the LDS image
+    // of buffer `buf`
+    auto rd_k = [&](const int buf, const int s, const int kt) {
+        return *reinterpret_cast<const V8*>(kaddr[s] + buf * TILE + kt * 32 * HD * 2);
+    };
+    // V^T operand of O^T += V^T P^T for (kt, sp, dt) through the transposing LDS read
+    auto rd_v = [&](const int buf, const int i) {
+        const int kt = i / (2 * ND), sp = (i / ND) & 1, dt = i % ND;
+        const char* b = smem + buf * TILE + (32 * kt + 16 * sp) * HD * 2;
+        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[0][dt]));
+        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[1][dt]));
+        const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+        return __builtin_bit_cast(V8, av);
+    };
+    // score transforms of values [v0, v0 + n) (flattened st[kt][r], v = 16 kt + r); masking
+    // only where a window edge crosses the tile
+    auto transform_part = [&](f32x16 (&st)[2], const int n0, const bool need_mask, const int v0,
+                              const int n) {
+#pragma unroll
+        for (int v = v0; v < v0 + n; ++v) {
+            const int kt = v >> 4, r = v & 15;
+            const int key = n0 + 4 * hh + 32 * kt + (r & 3) + 8 * (r >> 2);
+            if (FEAT && p.softcap_pre > 0.f) st[kt][r] = fast_tanh(st[kt][r] * p.softcap_pre);
+            if (FEAT && p.alibi) st[kt][r] -= alibi_w * (float)abs(pos + diag - key);
+            if (need_mask && (key >= my_lr || key < my_ll)) st[kt][r] = -INFINITY;
+        }
+    };
+    // Exact lazy rescale: only when some row of this wave raised its running max (the O^T
+    // rescale is a 64-register VALU pass; after the first tiles it is rare).
+    auto raise_max = [&](const float mx) {
+        const float m_new = fmaxf(m_run, mx);
+        if (__any(m_new > m_run)) {
+            const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
+            const float alpha = fast_exp2(m_run * c - mref);
+            l_run *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+            m_run = m_new;
+        }
+    };
+    // P = exp2(S c - m c) -> T (the B operand of the PV product) for values [v0, v0 + n);
+    // the row sum accumulates the rounded P pairs (v_dot2c against ones, two chains): the
+    // normaliser is then exactly the sum of the weights the PV MFMA multiplies.
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef typename DT<T>::v2 T2;
+    auto exp_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], const f2 m2, float (&rs)[2],
+                        const int v0, const int n) {
+        const f2 c2 = {c, c};
+#pragma unroll
+        for (int v = v0; v < v0 + n; v += 2) {
+            const int kt = v >> 4, r = v & 15;
+            f2 x = {st[kt][r], st[kt][r + 1]};
+            x = __builtin_elementwise_fma(x, c2, -m2);
+            const T2 e = {(T)fast_exp2(x[0]), (T)fast_exp2(x[1])};
+            pb[2 * kt + (r >> 3)][r & 7] = e[0];
+            pb[2 * kt + (r >> 3)][(r & 7) + 1] = e[1];
+            rs[(v >> 1) & 1] = DT<T>::sum2(e, rs[(v >> 1) & 1]);
+        }
+    };
+    auto exp_ref = [&]() {
+        const float mref = (m_run == -INFINITY) ? 0.f : m_run * c;
+        return f2{mref, mref};
+    };
+    // S^T = K Q^T (LDS reads one k-step ahead of the MFMAs)
+    auto qk = [&](const int ks, f32x16 (&st)[2]) {
+        st[0] = f32x16{};
+        st[1] = f32x16{};
+        V8 a0 = rd_k(ks, 0, 0), a1 = rd_k(ks, 0, 1);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            V8 n0 = a0, n1 = a1;
+            if (s + 1 < NS) { n0 = rd_k(ks, s + 1, 0); n1 = rd_k(ks, s + 1, 1); }
+            st[0] = DT<T>::mfma32(a0, qf[s], st[0]);
+            st[1] = DT<T>::mfma32(a1, qf[s], st[1]);
+            a0 = n0;
+            a1 = n1;
+        }
+    };
+    // O^T += V^T P^T (V^T reads one MFMA ahead)
+    constexpr int NPV = 4 * ND;                 // PV MFMAs per tile
+    auto pv = [&](const int vs, const V8 (&pb)[4]) {
+        V8 a = rd_v(vs, 0);
+#pragma unroll
+        for (int i = 0; i < NPV; ++i) {
+            V8 nx = a;
+            if (i + 1 < NPV) nx = rd_v(vs, i + 1);
+            acc_o[i % ND] = DT<T>::mfma32(a, pb[i / ND], acc_o[i % ND]);
+            a = nx;
+        }
+    };
+    auto row_max = [&](const f32x16 (&st)[2]) {
+        float mx = st[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
+        return wave_max_halves(mx);
+    };
+    auto exp_tile = [&](const f32x16 (&st)[2], V8 (&pb)[4]) {
+        float rs[2] = {0.f, 0.f};
+        exp_part(st, pb, exp_ref(), rs, 0, 32);
+        l_run += rs[0] + rs[1];
+    };
+
+    // ---- tiles that need per-wave masking / skipping: one tile in flight, two LDS buffers
+    auto masked_range = [&](const int lo, const int hi) {
+        if (lo >= hi) return;
+        load_to(lo, kr, vr);
+        store_from(0, kr, vr);
+        // Retire every outstanding load (Q fragments included) here: otherwise the loop-header
+        // merge of the waitcnt scoreboard makes the first QK^T MFMA of EVERY iteration wait
+        // vmcnt(0), i.e. drain the next tile's prefetch (vmcnt=0, expcnt=7, lgkmcnt=15).
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        int buf = 0;
+        for (int nb = lo; nb < hi; ++nb) {
+            const bool more = nb + 1 < hi;
+            if (more) load_to(nb + 1, kr, vr);
+            const int n0 = nb * kBlockN;
+            const bool active = wave_ok && n0 < w_lr_max && n0 + kBlockN > w_ll_min;
+            if (active) {
+                f32x16 st[2];
+                qk(buf, st);
+                transform_part(st, n0, (n0 + kBlockN > w_lr_min) || (n0 < w_ll_max), 0, 32);
+                raise_max(row_max(st));
+                V8 pb[4];
+                exp_tile(st, pb);
+                pv(buf, pb);
+            }
+            if (more) store_from(buf ^ 1, kr, vr);
+            __syncthreads();
+            buf ^= 1;
+        }
+    };
+
+    // ---- tiles every row of the workgroup sees in full: two-stage software pipeline.
+    // Step j issues QK^T of tile j+1 beside the softmax VALU of tile j, then PV of tile j beside
+    // the row max of tile j+1 (T15): the MFMA pipe always has independent work while the VALU
+    // finishes a tile.  Three LDS buffers rotate (K of j+1 | V of j | tile j+2 being written),
+    // one barrier per tile; the buffer indices are compile-time in the 3x unrolled loop.
+    auto pipe_range = [&](const int lo, const int hi) {
+        u32x4 kr2[NLD], vr2[NLD];
+        load_to(lo, kr, vr);
+        load_to(lo + 1, kr2, vr2);
+        store_from(0, kr, vr);
+        store_from(1, kr2, vr2);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __syncthreads();
+        f32x16 st[2];
+        qk(0, st);
+        transform_part(st, lo * kBlockN, false, 0, 32);
+        raise_max(row_max(st));
+        const int nsteps = hi - lo - 1;
+        auto step = [&](auto KB, auto VB, auto WB, const int j) {
+            constexpr int kb = decltype(KB)::value, vb = decltype(VB)::value, wb = decltype(WB)::value;
+            constexpr int ks = kb, vs = vb;
+            load_to((p.dbg & 1) ? lo : j + 2, kr, vr);   // past `hi`: harmless (zero / clamped) rows
+            if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+            // phase a: S_{j+1} = K_{j+1} Q^T on the MFMA pipe, P_j = exp(S_j) on the VALU
+            f32x16 sn[2] = {f32x16{}, f32x16{}};
+            V8 pb[4];
+            const f2 m2 = exp_ref();
+            float rs[2] = {0.f, 0.f};
+            constexpr int EV = 32 / (2 * NS);     // exp values per QK^T MFMA
+            V8 a0 = rd_k(ks, 0, 0), a1 = rd_k(ks, 0, 1);
+            V8 va, vb_;                           // V^T operands read two MFMAs ahead
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                const V8 a0 = *reinterpret_cast<const V8*>(ks + koff[s]);
-                const V8 a1 = *reinterpret_cast<const V8*>(ks + 32 * HD * 2 + koff[s]);
-                st[0] = DT<T>::mfma32(a0, qf[s], st[0]);
-                st[1] = DT<T>::mfma32(a1, qf[s], st[1]);
+                V8 n0 = a0, n1 = a1;
+                if (s + 1 < NS) { n0 = rd_k(ks, s + 1, 0); n1 = rd_k(ks, s + 1, 1); }
+                else { va = rd_v(vs, 0); vb_ = rd_v(vs, 1); }
+                sn[0] = DT<T>::mfma32(a0, qf[s], sn[0]);
+                exp_part(st, pb, m2, rs, (2 * s) * EV, EV);
+                sn[1] = DT<T>::mfma32(a1, qf[s], sn[1]);
+                exp_part(st, pb, m2, rs, (2 * s + 1) * EV, EV);
+                a0 = n0;
+                a1 = n1;
+                if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             }
-            // ---- score transforms + masking (only where a window edge crosses the tile)
-            if (FEAT && p.softcap_pre > 0.f) {
+            l_run += rs[0] + rs[1];
+            // phase b: O += V_j^T P_j on the MFMA pipe, transform + row max of S_{j+1} on the VALU
+            constexpr int MV = 32 / NPV;          // score values per PV MFMA
+            float mx = -INFINITY;
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
+            for (int i = 0; i < NPV; ++i) {
+                V8 nx = vb_;
+                if (i + 2 < NPV) nx = rd_v(vs, i + 2);
+                acc_o[i % ND] = DT<T>::mfma32(va, pb[i / ND], acc_o[i % ND]);
+                transform_part(sn, (j + 1) * kBlockN, false, i * MV, MV);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) st[kt][r] = fast_tanh(st[kt][r] * p.softcap_pre);
+                for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
+                va = vb_;
+                vb_ = nx;
+                if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             }
-            const int keyb = n0 + 4 * hh;
-            if (FEAT && p.alibi) {
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int key = keyb + 32 * kt + (r & 3) + 8 * (r >> 2);
-                        st[kt][r] -= alibi_w * (float)abs(pos + diag - key);
-                    }
+            raise_max(wave_max_halves(mx));
+            st[0] = sn[0];
+            st[1] = sn[1];
+            if (!(p.dbg & 2)) {
+                store_from(wb, kr, vr);
+                __syncthreads();
             }
-            const bool need_mask = (n0 + kBlockN > w_lr_min) || (n0 < w_ll_max);
-            if (need_mask) {
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int key = keyb + 32 * kt + (r & 3) + 8 * (r >> 2);
-                        if (key >= my_lr || key < my_ll) st[kt][r] = -INFINITY;
-                    }
-            }
-            // ---- online softmax (lane-local row + one half swap)
-            float mx = st[0][0];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
-            mx = wave_max_halves(mx);
-            const float m_new = fmaxf(m_run, mx);
-            const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
-            // Exact lazy rescale: only when some row of this wave raised its running max
-            // (the O^T rescale is a 64-register VALU pass; after the first tiles it is rare).
-            if (__any(m_new > m_run)) {
-                const float alpha = fast_exp2(m_run * c - mref);
-                l_run *= alpha;
-#pragma unroll
-                for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
-                m_run = m_new;
-            }
-            float rs[4] = {0.f, 0.f, 0.f, 0.f};   // 4 independent chains, not one 32-long
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float e = fast_exp2(fmaf(st[kt][r], c, -mref));
-                    st[kt][r] = e;
-                    rs[r & 3] += e;
-                }
-            l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
-            // ---- O^T += V^T P^T : P accumulator registers are the B operand as they stand
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-                for (int sp = 0; sp < 2; ++sp) {
-                    V8 pb;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) pb[j] = (T)st[kt][8 * sp + j];
-                    const int rbase = (32 * kt + 16 * sp) * HD * 2;
-#pragma unroll
-                    for (int dt = 0; dt < ND; ++dt) {
-                        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_s16x4*)(vs + rbase + voff[0][dt]));
-                        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_s16x4*)(vs + rbase + voff[1][dt]));
-                        const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-                        acc_o[dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb, acc_o[dt]);
-                    }
-                }
-            }
+        };
+        typedef std::integral_constant<int, 0> I0;
+        typedef std::integral_constant<int, 1> I1;
+        typedef std::integral_constant<int, 2> I2;
+        int r = 0;
+        while (r < nsteps) {
+            step(I1{}, I0{}, I2{}, lo + r);
+            if (++r >= nsteps) break;
+            step(I2{}, I1{}, I0{}, lo + r);
+            if (++r >= nsteps) break;
+            step(I0{}, I2{}, I1{}, lo + r);
+            ++r;
         }
-        if (more) store_tile(buf ^ 1);
+        // drain: the last tile's softmax and PV
+        V8 pb[4];
+        exp_tile(st, pb);
+        const int vb = nsteps % 3;
+        pv(vb, pb);
         __syncthreads();
-        buf ^= 1;
+    };
+
+    // Key tiles that every row of the workgroup sees in full (no mask, every wave active).
+    int f_lo = nb_hi, f_hi = nb_hi;
+    if (p.pipe) {
+        const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
+        f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
+        f_hi = min(nb_hi, lr_min / kBlockN);
+        if (f_hi - f_lo < 2) f_lo = f_hi = nb_hi;
+    }
+    if (p.prio_hi && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    // one call site per range kind: [nb_lo, f_lo) masked, [f_lo, f_hi) pipelined, [f_hi, nb_hi)
+    // masked
+#pragma unroll 1
+    for (int part = 0; part < 2; ++part) {
+        if (part == 1 && f_lo < f_hi) pipe_range(f_lo, f_hi);
+        masked_range(part == 0 ? nb_lo : f_hi, part == 0 ? f_lo : nb_hi);
     }
 
     // ---- epilogue: normalise, write O (or the split partial) and LSE
