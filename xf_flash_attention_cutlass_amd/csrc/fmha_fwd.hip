@@ -38,7 +38,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         const int slots = options().num_cus * options().fwd_persistent;
         if (items > slots) { pp.persistent = 1; grid = dim3(slots, 1, grid.z); }
     }
-    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(3 * 2 * kBlockN * HD * 2);
+    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(4 * 2 * kBlockN * HD * 2);
     void (*kern)(const FwdParams);
     if constexpr (PP) {
         const int sm = options().fwd_sched;

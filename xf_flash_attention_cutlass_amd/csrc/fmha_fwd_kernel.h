@@ -33,6 +33,15 @@ namespace xfa {
 #endif
 constexpr bool SCHED_FENCE = XFA_SCHED_FENCE;
 
+// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
 // One work item = (batch x kv-head, query row block, split).
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
 __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const int bh,
@@ -43,7 +52,8 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     constexpr int CPR = HD / 8;                 // 16-byte chunks per K/V row
     constexpr int NLD = kBlockN * CPR / NT;     // chunks per thread per tile
     constexpr int TILE = kBlockN * HD * 2;      // bytes of one K (or V) tile
-    constexpr int VREG = 3 * TILE;              // LDS: K tiles of buffers 0..2, then V tiles
+    constexpr int NBUF = 4;                     // LDS buffers (K and V tile each)
+    constexpr int VREG = NBUF * TILE;           // LDS: K tiles of buffers 0..3, then V tiles
     constexpr int NS = HD / 16;                 // k-steps of the QK^T product
     constexpr int ND = HD / 32;                 // 32-wide d tiles of O^T
     static_assert(NLD >= 1 && (NT % CPR) == 0, "tile/thread geometry");
@@ -350,28 +360,90 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         }
     };
 
+    // V^T operand through inline-asm transposing reads: the compiler's waitcnt pass treats
+    // the ds_read_tr builtin as aliasing every in-flight LDS-DMA and would drain the DMA queue
+    // (vmcnt(0)) before it; the asm reads are covered by explicit lgkmcnt waits instead.
+    // Byte offset OFF (buffer + row block) is an immediate.
+    int vaddr[2][ND];
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) vaddr[part][dt] = (int)(size_t)(smem) + voff[part][dt];
+    auto rd_v_asm = [&](auto OFF, const int dt) {
+        constexpr int off = decltype(OFF)::value;
+        s16x4 t0, t1;
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t0) : "v"(vaddr[0][dt]), "i"(off));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t1) : "v"(vaddr[1][dt]), "i"(off));
+        const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+        return __builtin_bit_cast(V8, av);
+    };
+    auto lgkm_wait = [&](auto N) {
+        constexpr int n = decltype(N)::value;
+        __builtin_amdgcn_s_waitcnt(0xC07F | (n << 8));
+        // the MFMA consuming the asm-read registers must not be scheduled above the wait
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
     // ---- tiles every row of the workgroup sees in full: two-stage software pipeline.
     // Step j issues QK^T of tile j+1 beside the softmax VALU of tile j, then PV of tile j beside
     // the row max of tile j+1 (T15): the MFMA pipe always has independent work while the VALU
-    // finishes a tile.  Three LDS buffers rotate (K of j+1 | V of j | tile j+2 being written),
-    // one barrier per tile; the buffer indices are compile-time in the 3x unrolled loop.
+    // finishes a tile.  K/V tiles stream straight into LDS (buffer_load ... lds, no staging
+    // registers) three tiles ahead through NBUF = 4 rotating buffers: at step j buffer
+    // (j+1)%4 holds K of j+1, j%4 holds V of j, and tiles j+2 (landing) and j+3 (issued now)
+    // are in flight.  One raw s_barrier per tile, preceded by a counted vmcnt that retires
+    // exactly tile j+2.  The LDS image is the same swizzled image the register-staged path
+    // writes: lane l of a wave-instruction lands at +16 l, so it fetches the global chunk
+    // (l % CPR) ^ swz(row) of its row.
+    constexpr int RPI = 64 / CPR;                  // tile rows per DMA wave-instruction
+    constexpr int IPW = kBlockN / RPI / NW;        // DMA wave-instructions per wave per K (V) tile
+    static_assert(IPW >= 1 && IPW * RPI * NW == kBlockN, "DMA geometry");
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    int dma_k[IPW], dma_v[IPW];                    // per-lane byte offsets within a tile
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+        const int r = (wave * IPW + i) * RPI + lane / CPR;
+        const int cch = (lane % CPR) ^ swz<HD>(r);
+        const bool ok = cch * 8 < p.d;
+        dma_k[i] = ok ? r * (int)p.k_row * 2 + cch * 16 : kOOB;
+        dma_v[i] = ok ? r * (int)p.v_row * 2 + cch * 16 : kOOB;
+    }
+    typedef __attribute__((address_space(3))) void lds_void;
+    auto dma_tile = [&](const int nb, const int buf) {
+        const int kso = nb * kBlockN * (int)p.k_row * 2, vso = nb * kBlockN * (int)p.v_row * 2;
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) {
+            const int g = wave_u * IPW + i;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                krs, (lds_void*)(smem + buf * TILE + g * 1024), 16, dma_k[i], kso, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                vrs, (lds_void*)(smem + VREG + buf * TILE + g * 1024), 16, dma_v[i], vso, 0, 0);
+        }
+    };
+    // counted vmcnt (the DMA writes are invisible to the compiler's waitcnt tracking) + a
+    // barrier that the compiler may not move memory operations across
+    constexpr int NDMA = 2 * IPW;                  // vmem instructions per tile per wave
+    auto publish = [&](const bool one_in_flight) {
+        if (one_in_flight) __builtin_amdgcn_s_waitcnt(0x0F70 | NDMA);
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
     auto pipe_range = [&](const int lo, const int hi) {
-        u32x4 kr2[NLD], vr2[NLD];
-        load_to(lo, kr, vr);
-        load_to(lo + 1, kr2, vr2);
-        store_from(0, kr, vr);
-        store_from(1, kr2, vr2);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        __syncthreads();
+        dma_tile(lo, 0);
+        dma_tile(lo + 1, 1);
+        const bool third = lo + 2 < hi;
+        if (third) dma_tile(lo + 2, 2);
+        publish(third);
         f32x16 st[2];
         qk(0, st);
         transform_part(st, lo * kBlockN, false, 0, 32);
         raise_max(row_max(st));
         const int nsteps = hi - lo - 1;
         auto step = [&](auto KB, auto VB, auto WB, const int j) {
-            constexpr int kb = decltype(KB)::value, vb = decltype(VB)::value, wb = decltype(WB)::value;
-            constexpr int ks = kb, vs = vb;
-            load_to((p.dbg & 1) ? lo : j + 2, kr, vr);   // past `hi`: harmless (zero / clamped) rows
+            constexpr int ks = decltype(KB)::value, vs = decltype(VB)::value, wb = decltype(WB)::value;
+            const bool issue = j + 3 < hi;
+            if (issue) dma_tile(j + 3, wb);
             if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             // phase a: S_{j+1} = K_{j+1} Q^T on the MFMA pipe, P_j = exp(S_j) on the VALU
             f32x16 sn[2] = {f32x16{}, f32x16{}};
@@ -380,12 +452,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             float rs[2] = {0.f, 0.f};
             constexpr int EV = 32 / (2 * NS);     // exp values per QK^T MFMA
             V8 a0 = rd_k(ks, 0, 0), a1 = rd_k(ks, 0, 1);
-            V8 va, vb_;                           // V^T operands read two MFMAs ahead
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
                 V8 n0 = a0, n1 = a1;
                 if (s + 1 < NS) { n0 = rd_k(ks, s + 1, 0); n1 = rd_k(ks, s + 1, 1); }
-                else { va = rd_v(vs, 0); vb_ = rd_v(vs, 1); }
                 sn[0] = DT<T>::mfma32(a0, qf[s], sn[0]);
                 exp_part(st, pb, m2, rs, (2 * s) * EV, EV);
                 sn[1] = DT<T>::mfma32(a1, qf[s], sn[1]);
@@ -395,52 +465,63 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             }
             l_run += rs[0] + rs[1];
-            // phase b: O += V_j^T P_j on the MFMA pipe, transform + row max of S_{j+1} on the VALU
+            // phase b: O += V_j^T P_j on the MFMA pipe, transform + row max of S_{j+1} on the
+            // VALU; V^T read two MFMAs ahead (asm reads, explicit lgkmcnt)
             constexpr int MV = 32 / NPV;          // score values per PV MFMA
+            auto voffs = [&](auto I) {             // immediate offset of PV operand I
+                constexpr int i = decltype(I)::value;
+                return std::integral_constant<int, vs * TILE + (32 * (i / (2 * ND)) + 16 * ((i / ND) & 1)) * HD * 2>{};
+            };
             float mx = -INFINITY;
-#pragma unroll
-            for (int i = 0; i < NPV; ++i) {
-                V8 nx = vb_;
-                if (i + 2 < NPV) nx = rd_v(vs, i + 2);
-                acc_o[i % ND] = DT<T>::mfma32(va, pb[i / ND], acc_o[i % ND]);
+            V8 ring[3];
+            ring[0] = rd_v_asm(voffs(std::integral_constant<int, 0>{}), 0);
+            ring[1] = rd_v_asm(voffs(std::integral_constant<int, 1>{}), 1 % ND);
+            static_for<NPV>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if constexpr (i + 2 < NPV) {
+                    ring[(i + 2) % 3] = rd_v_asm(voffs(std::integral_constant<int, i + 2>{}), (i + 2) % ND);
+                    lgkm_wait(std::integral_constant<int, 4>{});
+                } else if constexpr (i + 1 < NPV) {
+                    lgkm_wait(std::integral_constant<int, 2>{});
+                } else {
+                    lgkm_wait(std::integral_constant<int, 0>{});
+                }
+                acc_o[i % ND] = DT<T>::mfma32(ring[i % 3], pb[i / ND], acc_o[i % ND]);
                 transform_part(sn, (j + 1) * kBlockN, false, i * MV, MV);
 #pragma unroll
                 for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
-                va = vb_;
-                vb_ = nx;
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
-            }
+            });
             raise_max(wave_max_halves(mx));
             st[0] = sn[0];
             st[1] = sn[1];
-            if (!(p.dbg & 2)) {
-                store_from(wb, kr, vr);
-                __syncthreads();
-            }
+            publish(issue);                       // tile j+2 landed everywhere
         };
         typedef std::integral_constant<int, 0> I0;
         typedef std::integral_constant<int, 1> I1;
         typedef std::integral_constant<int, 2> I2;
+        typedef std::integral_constant<int, 3> I3;
         int r = 0;
         while (r < nsteps) {
-            step(I1{}, I0{}, I2{}, lo + r);
+            step(I1{}, I0{}, I3{}, lo + r);
             if (++r >= nsteps) break;
             step(I2{}, I1{}, I0{}, lo + r);
             if (++r >= nsteps) break;
-            step(I0{}, I2{}, I1{}, lo + r);
+            step(I3{}, I2{}, I1{}, lo + r);
+            if (++r >= nsteps) break;
+            step(I0{}, I3{}, I2{}, lo + r);
             ++r;
         }
         // drain: the last tile's softmax and PV
         V8 pb[4];
         exp_tile(st, pb);
-        const int vb = nsteps % 3;
-        pv(vb, pb);
+        pv(nsteps & 3, pb);
         __syncthreads();
     };
 
     // Key tiles that every row of the workgroup sees in full (no mask, every wave active).
     int f_lo = nb_hi, f_hi = nb_hi;
-    if (p.pipe) {
+    if (p.pipe && !paged && !kv8) {
         const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
         f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
         f_hi = min(nb_hi, lr_min / kBlockN);
