@@ -211,7 +211,7 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_sched")) { options().fwd_sched = value; return 0; }
     if (!strcmp(name, "fwd_store8")) { options().fwd_store8 = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
-    if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     fail(1, "unknown option '%s'", name);
     return -1;

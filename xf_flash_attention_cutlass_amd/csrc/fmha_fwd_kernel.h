@@ -429,7 +429,11 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    auto pipe_range = [&](const int lo, const int hi) {
+    // Tiles [lo, hm) need no mask; tiles [hm, hi) (the causal diagonal / right window edge /
+    // ragged end) are masked in registers on the way through the same pipeline (a wave whose
+    // rows cannot see such a tile computes zeros for it instead of branching out of the
+    // interleaved schedule).
+    auto pipe_range = [&](const int lo, const int hm, const int hi) {
         dma_tile(lo, 0);
         dma_tile(lo + 1, 1);
         const bool third = lo + 2 < hi;
@@ -437,7 +441,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         publish(third);
         f32x16 st[2];
         qk(0, st);
-        transform_part(st, lo * kBlockN, false, 0, 32);
+        transform_part(st, lo * kBlockN, lo >= hm, 0, 32);
         raise_max(row_max(st));
         const int nsteps = hi - lo - 1;
         auto step = [&](auto KB, auto VB, auto WB, const int j) {
@@ -487,11 +491,22 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                     lgkm_wait(std::integral_constant<int, 0>{});
                 }
                 acc_o[i % ND] = DT<T>::mfma32(ring[i % 3], pb[i / ND], acc_o[i % ND]);
-                transform_part(sn, (j + 1) * kBlockN, false, i * MV, MV);
+                if (FEAT) transform_part(sn, (j + 1) * kBlockN, false, i * MV, MV);
 #pragma unroll
                 for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             });
+            if (j + 1 >= hm) {                    // edge tile: mask after the transforms
+                const int n0 = (j + 1) * kBlockN + 4 * hh;
+#pragma unroll
+                for (int v = 0; v < 32; ++v) {
+                    const int key = n0 + 32 * (v >> 4) + (v & 3) + 8 * ((v & 15) >> 2);
+                    if (key >= my_lr || key < my_ll) sn[v >> 4][v & 15] = -INFINITY;
+                }
+                mx = sn[0][0];
+#pragma unroll
+                for (int v = 1; v < 32; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
+            }
             raise_max(wave_max_halves(mx));
             st[0] = sn[0];
             st[1] = sn[1];
@@ -501,6 +516,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         typedef std::integral_constant<int, 1> I1;
         typedef std::integral_constant<int, 2> I2;
         typedef std::integral_constant<int, 3> I3;
+        // step r (tile j = lo + r) reads K of j+1 from buffer (r+1)%4 and V of j from r%4
         int r = 0;
         while (r < nsteps) {
             step(I1{}, I0{}, I3{}, lo + r);
@@ -519,22 +535,22 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         __syncthreads();
     };
 
-    // Key tiles that every row of the workgroup sees in full (no mask, every wave active).
+    // Key tiles: [nb_lo, f_lo) cross the left window edge (per-wave masked loop);
+    // [f_lo, f_hi) every row of the workgroup sees in full; [f_hi, nb_hi) cross the right
+    // window edge / the end of the keys.  The last two ranges run through the pipeline.
     int f_lo = nb_hi, f_hi = nb_hi;
     if (p.pipe && !paged && !kv8) {
         const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
         f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
-        f_hi = min(nb_hi, lr_min / kBlockN);
-        if (f_hi - f_lo < 2) f_lo = f_hi = nb_hi;
+        f_hi = max(f_lo, min(nb_hi, lr_min / kBlockN));
+        if (nb_hi - f_lo < 2 || (p.pipe == 2 && f_hi - f_lo < 2)) f_lo = f_hi = nb_hi;
     }
     if (p.prio_hi && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    // one call site per range kind: [nb_lo, f_lo) masked, [f_lo, f_hi) pipelined, [f_hi, nb_hi)
-    // masked
-#pragma unroll 1
-    for (int part = 0; part < 2; ++part) {
-        if (part == 1 && f_lo < f_hi) pipe_range(f_lo, f_hi);
-        masked_range(part == 0 ? nb_lo : f_hi, part == 0 ? f_lo : nb_hi);
-    }
+    // (fwd_pipe=2: edge tiles through the per-wave masked loop instead - A/B knob)
+    const int p_hi = (p.pipe == 2 && f_hi - f_lo >= 2) ? f_hi : nb_hi;
+    masked_range(nb_lo, f_lo);
+    if (f_lo < p_hi) pipe_range(f_lo, f_hi, p_hi);
+    masked_range(p_hi, nb_hi);
 
     // ---- epilogue: normalise, write O (or the split partial) and LSE
     const float l_full = wave_sum_halves(l_run);
