@@ -260,13 +260,15 @@ def _fp8_cache(x, scale, dt=torch.bfloat16):
 
 
 @pytest.mark.parametrize("num_splits", [1, 0, 3])
-@pytest.mark.parametrize("sq,hk", [(1, 8), (1, 2), (4, 2)])
+@pytest.mark.parametrize("sq,hk", [(1, 8), (1, 2), (4, 2), (16, 2)])
 @pytest.mark.parametrize("dtype", ["bfloat16", "float16"])
 def test_paged_fp8_cache(xfa, num_splits, sq, hk, dtype):
-    """fp8 (e4m3fn) paged cache == the bf16/fp16 path over the dequantised cache, bit for bit;
-    and within the kvcache tolerance of the oracle.  (No reference counterpart: the reference
-    has no fp8 cache — SURVEY §8d C5 is this build's extension, parity pinned by the
-    dequantised-cache equality, not by a reference fixture.)"""
+    """fp8 (e4m3fn) paged cache vs the oracle over the dequantised cache dt(f32(fp8) * scale),
+    within the kvcache tolerance.  (No reference counterpart: the reference has no fp8 cache —
+    SURVEY §8d C5 is this build's extension; parity pinned by the dequantised-cache oracle.)
+    sq * H/Hk <= 32 runs the decode kernel (scales applied in fp32 to S and O); sq = 16 runs the
+    general kernel, whose staging dequantises exactly like the reference cache would, so there
+    it must also equal the 16-bit path over the dequantised cache bit for bit."""
     torch.manual_seed(1)
     dt = _dtype(dtype)
     b, h, d, page, sk = 3, 8, 128, 16, 1000
@@ -283,8 +285,11 @@ def test_paged_fp8_cache(xfa, num_splits, sq, hk, dtype):
     outd, lsed = xfa.flash_attn_with_kvcache(q, kpd.to(DEV), vpd.to(DEV), cache_seqlens=seqlens,
                                              block_table=tab, num_splits=num_splits,
                                              return_softmax_lse=True)
-    assert torch.equal(out8, outd)
-    assert torch.equal(lse8, lsed)
+    if sq * h // hk > 32:
+        assert torch.equal(out8, outd)
+        assert torch.equal(lse8, lsed)
+    else:
+        assert (lse8 - lsed).abs().max().item() < 5e-3
     nblk = table.shape[1]
     kfull = kpd[table.long().flatten()].reshape(b, nblk * page, hk, d)[:, :sk]
     vfull = vpd[table.long().flatten()].reshape(b, nblk * page, hk, d)[:, :sk]
@@ -292,6 +297,75 @@ def test_paged_fp8_cache(xfa, num_splits, sq, hk, dtype):
     r, _ = orc.attention_ref(q.cpu(), kfull, vfull, None, kpm)
     pt, _ = orc.attention_ref(q.cpu(), kfull, vfull, None, kpm, upcast=False, reorder_ops=True)
     _assert_parity(out8, r, pt, mult=3.0, atol=1e-5, what="paged fp8")
+    _assert_parity(outd, r, pt, mult=3.0, atol=1e-5, what="paged dequantised")
+
+
+def test_paged_fp8_generic_staging_bitexact(xfa):
+    """With the decode kernel switched off, the general kernel's fp8 staging (dequantise while
+    staging) equals the 16-bit path over the dequantised cache bit for bit."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(3)
+    b, h, hk, d, page, sk = 2, 8, 2, 128, 16, 300
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    kp8, kpd = _fp8_cache(kp, 0.02)
+    vp8, vpd = _fp8_cache(vp, 0.03)
+    q = torch.randn(b, 1, h, d).bfloat16().to(DEV)
+    seqlens = torch.tensor([300, 77], dtype=torch.int32).to(DEV)
+    tab = table.to(DEV)
+    assert L.fmha_set_option(b"fwd_decode", 0) == 0
+    try:
+        o8 = xfa.flash_attn_with_kvcache(q, kp8.to(DEV), vp8.to(DEV), cache_seqlens=seqlens,
+                                         block_table=tab, k_scale=0.02, v_scale=0.03)
+        od = xfa.flash_attn_with_kvcache(q, kpd.to(DEV), vpd.to(DEV), cache_seqlens=seqlens,
+                                         block_table=tab)
+    finally:
+        L.fmha_set_option(b"fwd_decode", 1)
+    assert torch.equal(o8, od)
+
+
+@pytest.mark.parametrize("sq,h,hk,d", [(1, 32, 8, 128), (1, 8, 1, 64), (2, 16, 2, 128),
+                                       (1, 6, 6, 64), (3, 12, 1, 128)])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
+    """Decode shapes (sq * H/Hk <= 32) through mha_fwd (dense K/V) and through the paged cache,
+    against the oracle; the decode and general kernels agree to rounding."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(5)
+    b, sk = 3, 777
+    q = torch.randn(b, sq, h, d, dtype=dtype)
+    k = torch.randn(b, sk, hk, d, dtype=dtype)
+    v = torch.randn(b, sk, hk, d, dtype=dtype)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
+    r, _ = orc.attention_ref(q, k, v, causal=causal)
+    pt, _ = orc.attention_ref(q, k, v, causal=causal, upcast=False, reorder_ops=True)
+    _assert_parity(out, r, pt, what="decode dense")
+    assert L.fmha_set_option(b"fwd_decode", 0) == 0
+    try:
+        ref_gen = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
+    finally:
+        L.fmha_set_option(b"fwd_decode", 1)
+    assert (out.float() - ref_gen.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("window", [(64, 0), (100, 7), (-1, 5)])
+def test_decode_kernel_window_alibi_softcap(xfa, window):
+    torch.manual_seed(6)
+    b, sq, h, hk, d, sk = 2, 4, 16, 4, 128, 500
+    q = torch.randn(b, sq, h, d, dtype=torch.bfloat16)
+    k = torch.randn(b, sk, hk, d, dtype=torch.bfloat16)
+    v = torch.randn(b, sk, hk, d, dtype=torch.bfloat16)
+    slopes = torch.rand(b, h, dtype=torch.float32) * 0.3
+    bias = orc.alibi_bias(slopes, sq, sk, causal=False)
+    win = oracle_window(window, sk)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), window_size=window,
+                              alibi_slopes=slopes.to(DEV), softcap=15.0)
+    r, _ = orc.attention_ref(q, k, v, attn_bias=bias, window_size=win, softcap=15.0)
+    pt, _ = orc.attention_ref(q, k, v, attn_bias=bias, window_size=win, softcap=15.0,
+                              upcast=False, reorder_ops=True)
+    _assert_parity(out, r, pt, mult=5.0, what=f"decode window {window}")
 
 
 def test_paged_fp8_capi(xfa):

@@ -165,12 +165,26 @@ void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
 void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     const int n_blocks = (p.seqlen_k + kBlockN - 1) / kBlockN;
     int splits = num_splits_req;
-    if (p.cu_seqlens_q) splits = 1;  // varlen: single pass (the reference forces it too)
-    if (splits <= 0) {
+    // Decode: the whole GQA group of query rows fits one 32-row MFMA tile -> the split-KV
+    // decode kernel (every wave a split, fmha_decode_kernel.h); splits a multiple of 4.
+    p.decode = options().fwd_decode && !p.cu_seqlens_q && !p.cu_seqlens_k &&
+               p.seqlen_q * p.group <= 32 && hd_bucket(p.d) == p.d &&
+               (!p.block_table || p.page_size % 16 == 0);
+    if (p.decode) {
+        const int tiles = (p.seqlen_k + 31) / 32;
+        const int work = p.b * p.hk;
+        int zs = num_splits_req > 0 ? (num_splits_req + 3) / 4
+                                    : (2 * num_cus() + work - 1) / work;
+        zs = std::max(1, std::min(zs, std::max(1, tiles / 8)));
+        zs = std::min(zs, 32);
+        splits = 4 * zs;
+    } else if (p.cu_seqlens_q) {
+        splits = 1;  // varlen: single pass (the reference forces it too)
+    } else if (splits <= 0) {
         const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group);
         splits = num_splits_heuristic(work, num_cus() * 2, n_blocks, 128);
     }
-    splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
+    if (!p.decode) splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
     p.num_splits = splits;
     if (splits > 1) {
         const int hd = hd_bucket(p.d);
@@ -213,6 +227,7 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
     if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
+    if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
     fail(1, "unknown option '%s'", name);
     return -1;
 }

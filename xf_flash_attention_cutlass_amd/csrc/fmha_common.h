@@ -81,6 +81,7 @@ struct FwdParams {
     int n_mblocks;             // row blocks per (b, kv head) (persistent mode)
     int pipe;                  // 1: software-pipelined loop over the unmasked key tiles
     int dbg;                   // timing experiments only (results invalid when set)
+    int decode;                // 1: run fmha_decode_kernel (split-KV decode)
 };
 
 struct CombineParams {
@@ -174,6 +175,12 @@ __device__ __forceinline__ float wave_max_halves(float x) {
 __device__ __forceinline__ float wave_sum_halves(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// s_waitcnt immediate for gfx9: vmcnt(n) (6 bits, split [3:0] / [15:14]), expcnt and lgkmcnt
+// left unconstrained.
+__host__ __device__ constexpr int waitcnt_vm(int n) {
+    return (n & 0xF) | ((n >> 4) << 14) | 0x0F70;
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

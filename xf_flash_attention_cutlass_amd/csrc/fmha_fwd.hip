@@ -4,6 +4,7 @@
 // perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
 #include "fmha_fwd_kernel.h"
 #include "fmha_fwd_pp_kernel.h"
+#include "fmha_decode_kernel.h"
 #include "fmha_launch.h"
 
 #ifndef XFA_HD
@@ -21,6 +22,33 @@ typedef __bf16 elem_t;
 #else
 typedef _Float16 elem_t;
 #endif
+
+static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
+                                 void (*kern)(const CombineParams)) {
+    CombineParams cp;
+    cp.oaccum = p.oaccum;
+    cp.lseaccum = p.lseaccum;
+    cp.o = p.o;
+    cp.lse = p.lse;
+    cp.o_batch = p.o_batch; cp.o_row = p.o_row; cp.o_head = p.o_head;
+    cp.lse_batch = p.lse_batch; cp.lse_head = p.lse_head;
+    cp.b = p.b; cp.h = p.h; cp.seqlen_q = p.seqlen_q; cp.d = p.d; cp.hd = hd;
+    cp.num_splits = p.num_splits;
+    const int64_t crow = (int64_t)p.b * p.h * p.seqlen_q;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
+    return hipGetLastError();
+}
+
+template <int HD, typename T>
+static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
+    const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
+    dim3 grid(p.b * p.hk, p.num_splits / kDecWaves);
+    if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true>), grid, dim3(kDecWaves * 64), smem, st, p);
+    else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false>), grid, dim3(kDecWaves * 64), smem, st, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
+}
 
 template <int HD, typename T, int NW, bool PP>
 static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
@@ -70,22 +98,11 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
-
-    CombineParams cp;
-    cp.oaccum = p.oaccum;
-    cp.lseaccum = p.lseaccum;
-    cp.o = p.o;
-    cp.lse = p.lse;
-    cp.o_batch = p.o_batch; cp.o_row = p.o_row; cp.o_head = p.o_head;
-    cp.lse_batch = p.lse_batch; cp.lse_head = p.lse_head;
-    cp.b = p.b; cp.h = p.h; cp.seqlen_q = p.seqlen_q; cp.d = p.d; cp.hd = HD;
-    cp.num_splits = p.num_splits;
-    const int64_t crow = (int64_t)p.b * p.h * p.seqlen_q;
-    hipLaunchKernelGGL((fmha_combine_kernel<HD, T>), dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
-    return hipGetLastError();
+    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
 }
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
+    if (p.decode) return launch_decode<XFA_HD, elem_t>(p, st);
     if (options().fwd_pp && !p.kv_fp8) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
     if (options().fwd_waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8, false>(p, st);
     return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);

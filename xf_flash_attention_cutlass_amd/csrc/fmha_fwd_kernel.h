@@ -423,7 +423,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // barrier that the compiler may not move memory operations across
     constexpr int NDMA = 2 * IPW;                  // vmem instructions per tile per wave
     auto publish = [&](const bool one_in_flight) {
-        if (one_in_flight) __builtin_amdgcn_s_waitcnt(0x0F70 | NDMA);
+        if (one_in_flight) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NDMA));
         else __builtin_amdgcn_s_waitcnt(0x0F70);
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();

@@ -18,6 +18,7 @@ struct Options {
     int fwd_persistent = 1;   // persistent grid (workgroups per CU; 0 = one workgroup per item)
     int fwd_pipe = 1;         // software-pipelined loop over the unmasked key tiles
     int fwd_dbg = 0;          // timing experiments only (results invalid when set)
+    int fwd_decode = 1;       // split-KV decode kernel when seqlen_q * H/Hk <= 32
     int num_cus = 256;        // filled by the C ABI from the device
 };
 Options& options();
