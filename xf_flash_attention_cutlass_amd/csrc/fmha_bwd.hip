@@ -41,7 +41,7 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
         attr_done = true;
     }
     const dim3 grid(p.b * p.hk, (p.seqlen_k + kBwdBlockN - 1) / kBwdBlockN);
-    hipLaunchKernelGGL(kern, grid, dim3(kBwdWaves * 64), smem, st, p);
+    hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, p);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((fmha_bwd_convert_kernel<HD, T>), dim3(blocks), dim3(256), 0, st, p, total_rows);

@@ -24,9 +24,15 @@
 
 namespace xfa {
 
-constexpr int kBwdWaves = 4;                 // waves per workgroup (one per SIMD)
-constexpr int kBwdKeysPerWave = 64;          // keys owned by one wave (2 x 32-key subtiles)
-constexpr int kBwdBlockN = kBwdKeysPerWave * kBwdWaves;   // keys per workgroup
+#ifndef XFA_BWD_WAVES
+#define XFA_BWD_WAVES 8
+#endif
+// Waves per workgroup.  D = 128: 8 waves x 32 keys, two waves per SIMD (256 registers each)
+// so one wave's LDS / global waits hide behind the other's MFMAs.  D = 64 (or
+// XFA_BWD_WAVES=4): 4 waves x 64 keys, one wave per SIMD with 512 registers (a 32-row D=64
+// Q tile has too few 16-byte chunks for 512 threads).
+template <int HD> constexpr int bwd_waves() { return HD >= 128 ? XFA_BWD_WAVES : 4; }
+constexpr int kBwdBlockN = 256;              // keys per workgroup
 constexpr int kBwdBlockM = 32;               // query rows per tile
 
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
@@ -114,9 +120,10 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
 
 // ---------------------------------------------------------------- main ---------------------
 template <int HD, typename T, bool MASK, bool FEAT>
-__global__ void __launch_bounds__(kBwdWaves * 64, 1) fmha_bwd_kernel(const BwdParams p) {
+__global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
     using V8 = typename DT<T>::v8;
-    constexpr int NW = kBwdWaves;
+    constexpr int NW = bwd_waves<HD>();
+    constexpr int kBwdKeysPerWave = kBwdBlockN / NW;   // keys owned by one wave
     constexpr int NT = NW * 64;
     constexpr int KS = kBwdKeysPerWave / 32;     // 32-key subtiles per wave
     constexpr int BN = kBwdBlockN;
