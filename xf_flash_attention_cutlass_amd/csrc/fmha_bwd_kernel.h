@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const int lr = lane & 31;
     const int hh = lane >> 5;
 
@@ -199,23 +199,39 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     constexpr int LROW_STEP = NT / CPR;
     const bool ld_ok = lcol * 8 < p.d;
     uint4 qreg[QLD], doreg[QLD];
+    // LSE (lanes 0-31, pre-multiplied by log2e) and D = rowsum(dO*O) (lanes 32-63) of the
+    // tile's 32 rows: one load per lane, prefetched with Q/dO, fetched by ds_bpermute
+    float lsd_next = 0.f;
     auto load_q = [&](int it) {
         const int g = it / ntiles;
         const int tt = it - g * ntiles;
         const int head = hk_i * G + g;
+        {
+            const int pos = (t_lo + tt) * BQ + lr;
+            const bool ok = pos < sq;
+            const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off +
+                               (ok ? pos : 0);
+            const float x = (hh ? p.dsum : p.lse)[li];
+            lsd_next = hh ? (ok ? x : 0.f) : (ok ? x * kLog2e : INFINITY);
+        }
+        // buffer loads over this head's rows [q0, sq): rows past the end and padded head-dim
+        // chunks read as zeros (no branches)
+        const int q0n = (t_lo + tt) * BQ;
+        const T* qb = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
+                      (int64_t)(q_off + q0n) * p.q_row + (int64_t)head * p.q_head;
+        const T* gb = reinterpret_cast<const T*>(p.dout) + (int64_t)bidx * p.do_batch +
+                      (int64_t)(q_off + q0n) * p.do_row + (int64_t)head * p.do_head;
+        const int nrows = max(0, sq - q0n);
+        const __amdgpu_buffer_rsrc_t qrs = make_rsrc(qb, (uint32_t)(nrows * p.q_row * 2));
+        const __amdgpu_buffer_rsrc_t grs = make_rsrc(gb, (uint32_t)(nrows * p.do_row * 2));
 #pragma unroll
         for (int i = 0; i < QLD; ++i) {
-            const int pos = (t_lo + tt) * BQ + lrow + i * LROW_STEP;
-            qreg[i] = make_uint4(0, 0, 0, 0);
-            doreg[i] = make_uint4(0, 0, 0, 0);
-            if (ld_ok && pos < sq) {
-                const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
-                              (int64_t)(q_off + pos) * p.q_row + (int64_t)head * p.q_head + lcol * 8;
-                const T* gp = reinterpret_cast<const T*>(p.dout) + (int64_t)bidx * p.do_batch +
-                              (int64_t)(q_off + pos) * p.do_row + (int64_t)head * p.do_head + lcol * 8;
-                qreg[i] = *reinterpret_cast<const uint4*>(qp);
-                doreg[i] = *reinterpret_cast<const uint4*>(gp);
-            }
+            const int r = lrow + i * LROW_STEP;
+            const int qo = ld_ok ? r * (int)p.q_row * 2 + lcol * 16 : kOOB;
+            const int go = ld_ok ? r * (int)p.do_row * 2 + lcol * 16 : kOOB;
+            const u32x4 a = buf_load16(qrs, qo), b = buf_load16(grs, go);
+            qreg[i] = make_uint4(a[0], a[1], a[2], a[3]);
+            doreg[i] = make_uint4(b[0], b[1], b[2], b[3]);
         }
     };
     auto store_q = [&]() {
@@ -227,12 +243,13 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         }
     };
 
-    // per-lane LDS offsets
-    int koff[NS], qoff[NS];
+    // per-lane LDS addresses (tile-relative constants fold into the ds_read offsets)
+    const char* kaddr[NS];
+    const char* qaddr[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        koff[s] = lds_off<HD>(wave * kBwdKeysPerWave + lr, 2 * s + hh);   // + 32*ks rows
-        qoff[s] = lds_off<HD>(lr, 2 * s + hh);
+        kaddr[s] = k_lds + lds_off<HD>(wave * kBwdKeysPerWave + lr, 2 * s + hh);   // + 32*ks rows
+        qaddr[s] = q_lds + lds_off<HD>(lr, 2 * s + hh);
     }
     const int q4 = (lane & 15) >> 2;
     int troff[2][ND];   // transposed reads of the Q / dO tile (A operand: rows q, column d)
@@ -270,9 +287,10 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
+    float lsd_cur = 0.f;
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible
-    if (n_iter > 0) { store_q(); }
+    if (n_iter > 0) { store_q(); lsd_cur = lsd_next; }
     __syncthreads();
 
     for (int it = 0; it < n_iter; ++it) {
@@ -280,6 +298,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         const int tt = it - g * ntiles;
         const int head = hk_i * G + g;
         const int q0 = (t_lo + tt) * BQ;
+        const float lsd = lsd_cur;
         if (it + 1 < n_iter) load_q(it + 1);
 
         // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
@@ -288,29 +307,34 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int ks = 0; ks < KS; ++ks) { s_acc[ks] = f32x16{}; dp_acc[ks] = f32x16{}; }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const V8 qa = *reinterpret_cast<const V8*>(q_lds + qoff[s]);
-            const V8 ga = *reinterpret_cast<const V8*>(do_lds + qoff[s]);
+            const V8 qa = *reinterpret_cast<const V8*>(qaddr[s]);
+            const V8 ga = *reinterpret_cast<const V8*>(qaddr[s] + QT_BYTES);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const V8 kb = *reinterpret_cast<const V8*>(k_lds + ks * 32 * HD * 2 + koff[s]);
-                const V8 vb = *reinterpret_cast<const V8*>(v_lds + ks * 32 * HD * 2 + koff[s]);
+                const V8 kb = *reinterpret_cast<const V8*>(kaddr[s] + ks * 32 * HD * 2);
+                const V8 vb = *reinterpret_cast<const V8*>(kaddr[s] + KT_BYTES + ks * 32 * HD * 2);
                 s_acc[ks] = DT<T>::mfma32(qa, kb, s_acc[ks]);
                 dp_acc[ks] = DT<T>::mfma32(ga, vb, dp_acc[ks]);
             }
         }
         // ---- P = exp2(S*c - LSE*log2e), dS = P * (dP - D)
-        const int64_t lrow_base = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off;
         float alibi_w = 0.f;
         if (FEAT && p.alibi) alibi_w = p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul;
+        // the window / key-range test only where this wave's 32 keys x the 32 rows cross an edge
+        const int kw0 = n0 + wave * kBwdKeysPerWave, kw1 = kw0 + kBwdKeysPerWave - 1;
+        bool need_mask = kw1 >= sk;
+        if (MASK && p.wr >= 0) need_mask = need_mask || kw1 >= q0 + diag + p.wr + 1;
+        if (MASK && p.wl >= 0) need_mask = need_mask || kw0 < q0 + BQ - 1 + diag - p.wl;
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             const int pos0 = q0 + 8 * gq + 4 * hh;
             float lse4[4], d4[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const bool ok = pos0 + i < sq;
-                lse4[i] = ok ? p.lse[lrow_base + pos0 + i] * kLog2e : INFINITY;
-                d4[i] = ok ? p.dsum[lrow_base + pos0 + i] : 0.f;
+                // row 8gq + 4hh + i of this tile: lane (row) holds its LSE, lane 32 + row its D
+                const int src = 4 * (8 * gq + 4 * hh + i);
+                lse4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(lsd)));
+                d4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(lsd)));
             }
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
@@ -324,12 +348,12 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 if (FEAT && p.softcap_on) { w = fast_tanh(w * p.softcap_pre); dcap = 1.f - w * w; }
                 if (FEAT && p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
                 float pr = fast_exp2(fmaf(w, c, -lse4[i]));
-                bool keep = key < sk;
-                if (MASK) {
-                    if (p.wr >= 0) keep = keep && key < pos + diag + p.wr + 1;
-                    if (p.wl >= 0) keep = keep && key >= pos + diag - p.wl;
+                if (need_mask) {
+                    // visible keys of row pos: [lo, hi) -> one unsigned compare
+                    const int hi = (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk;
+                    const int lo = (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0;
+                    pr = (unsigned)(key - lo) < (unsigned)max(hi - lo, 0) ? pr : 0.f;
                 }
-                pr = keep ? pr : 0.f;
                 s_acc[ks][r] = pr;
                 dp_acc[ks][r] = pr * (dp_acc[ks][r] - d4[i]) * dcap;
             }
@@ -392,19 +416,24 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                     dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
                 }
             }
-            float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head;
+            // buffer atomics over this (batch, head)'s rows [q0, sq): rows past the end and the
+            // padded head-dim columns fall outside the descriptor and are dropped (no branches)
+            const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+                              (int64_t)(q_off + q0) * p.acc_row;
+            const __amdgpu_buffer_rsrc_t qrs =
+                make_rsrc(qa, (uint32_t)(max(0, sq - q0) * p.acc_row * 4));
+            const int arow = (int)p.acc_row * 4;
 #pragma unroll
             for (int i = 0; i < NDQ; ++i) {
                 const int d = 16 * ((wave >> 1) * NDQ + i) + (lane & 15);
+                const int base = d < p.d ? (16 * mt + 4 * g16) * arow + d * 4 : kOOB;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int pos = q0 + 16 * mt + 4 * g16 + r;
-                    if (pos < sq && d < p.d)
-                        atomicAdd(qa + (int64_t)(q_off + pos) * p.acc_row + d, dq[i][r]);
-                }
+                for (int r = 0; r < 4; ++r)
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq[i][r], qrs, base + r * arow, 0, 0);
             }
         }
         if (it + 1 < n_iter) store_q();
+        lsd_cur = lsd_next;
         __syncthreads();
     }
 
