@@ -53,8 +53,8 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
 template <int HD, typename T, int NW, bool PP>
 static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     const bool mask = p.wl >= 0 || p.wr >= 0;
-    const bool feat = p.alibi || p.softcap_pre > 0.f || p.cu_seqlens_q || p.cu_seqlens_k ||
-                      p.seqused_k || p.block_table || p.num_splits > 1 || p.kv_fp8;
+    // FEAT: per-score transforms (ALiBi, softcap) and the paged / fp8 staging paths
+    const bool feat = p.alibi || p.softcap_pre > 0.f || p.block_table || p.kv_fp8;
     const int rows = p.seqlen_q * p.group;
     const int n_mb = (rows + NW * 32 - 1) / (NW * 32);
     dim3 grid(p.b * p.hk, n_mb, p.num_splits > 1 ? p.num_splits : 1);

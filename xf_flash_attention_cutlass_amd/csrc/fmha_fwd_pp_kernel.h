@@ -52,11 +52,9 @@ __global__ void __launch_bounds__(512, 2) fmha_fwd_pp_kernel(const FwdParams p) 
     const int split = blockIdx.z;
 
     int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
-    if (FEAT) {
-        if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
-        if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
-        if (p.seqused_k) sk = p.seqused_k[bidx];
-    }
+    if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
+    if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
+    if (p.seqused_k) sk = p.seqused_k[bidx];
     const int G = p.group;
     const int rows_total = sq * G;
     const int row0 = m_block * BM;
@@ -71,7 +69,7 @@ __global__ void __launch_bounds__(512, 2) fmha_fwd_pp_kernel(const FwdParams p) 
     const int n_hi = lim_r(pos_hi);
     int nb_lo = n_lo / kBlockN;
     int nb_hi = n_hi > n_lo ? (n_hi + kBlockN - 1) / kBlockN : nb_lo;
-    const bool is_split = FEAT && p.num_splits > 1;
+    const bool is_split = p.num_splits > 1;
     if (is_split) {
         const int per = (nb_hi - nb_lo + p.num_splits - 1) / p.num_splits;
         const int s_lo = nb_lo + split * per;
