@@ -573,6 +573,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     }
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
               (int64_t)(q_off + pos) * p.o_row + (int64_t)head * p.o_head;
+    if (p.dbg & 4) return;                 // timing experiment: no O / LSE stores
     if (p.store8) store_o_row8<T, ND>(orow, acc_o, inv, p.d, hh);
     else store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
     if (p.lse && hh == 0) {
