@@ -119,6 +119,26 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
                               int32_t kv_dtype, float k_scale, float v_scale, bool is_fp16,
                               hipStream_t stream);
 
+/* KV-cache append with optional rotary embedding: the write step of mha_fwd_kvcache with new
+ * k/v (export.cpp:1585-1669, kernel flash_fwd_kernel_hip.h:817-934 / rotary_hip.h:21-152 - never
+ * enabled by the reference's C path, csrc/paged_attn.cpp:513-525).  For each batch b and new
+ * token j: pos = cache_seqlens[b] + j; kcache/vcache slot (block_table[b][pos / page],
+ * pos % page) <- rotary(knew[b][j]) / vnew[b][j]; seqlens_out[b] = cache_seqlens[b] +
+ * seqlen_new.  With rotary_dim > 0 also q_out = rotary(q) at position cache_seqlens[b] + s
+ * (q_rotary_per_token, the causal/local case) or cache_seqlens[b] (otherwise).  rotary_cos /
+ * rotary_sin: [seqlen_ro, rotary_dim / 2] in q's dtype; interleaved = GPT-J pairs (2i, 2i+1),
+ * else GPT-NeoX halves (i, i + rotary_dim/2).  knew/vnew contiguous [b, seqlen_new, hk, d];
+ * caches contiguous [num_blocks, page, hk, d]; q/q_out contiguous [b, seqlen_q, h, d].
+ * Stream-ordered; run the attention (fmha_page_kvcache_fwd_ex with seqlens_out) after it. */
+void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const void* knew,
+                         const void* vnew, int32_t seqlen_new, const void* block_table,
+                         int32_t block_table_stride, int32_t page_block_size,
+                         const void* cache_seqlens, void* seqlens_out, const void* rotary_cos,
+                         const void* rotary_sin, int32_t rotary_dim, bool is_rotary_interleaved,
+                         bool q_rotary_per_token, int32_t batch_size, int32_t seqlen_q,
+                         int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                         bool is_fp16, hipStream_t stream);
+
 /* Dense backward: the C form of mha_bwd (export.cpp:948-1176, live twin flash_api_hip.cpp:
  * 815-1043), which the reference never built.  Inputs dout/q/k/v/out as the fwd layout,
  * softmax_lse fp32 [batch, heads, seqlen_q] from fmha_fwd; outputs dq [b,sq,h,d],

@@ -19,6 +19,12 @@ Functions and the reference lines they restate:
                            vendored; semantics as used at test.py:620-635:
                            4-tuple (x_unpad, indices, cu_seqlens int32, max_seqlen))
 * `block_kvcache`       -> `_generate_block_kvcache`       test.py:1597-1621
+* `apply_rotary`        -> flash_attn.layers.rotary.apply_rotary_emb (third-party, not
+                           vendored; semantics as used by the commented-out rotary branch of
+                           test_flash_attn_kvcache, test.py:1454-1486: GPT-NeoX halves or
+                           GPT-J interleaved pairs over the first rotary_dim features,
+                           positions seqlen_offsets[b] + s).  Parity for rotary is pinned only
+                           by this restatement (the reference never runs it).
 
 Pass rules (test.py:975, 1296, 1593-1594) live in `parity_ok`.
 """
@@ -32,7 +38,7 @@ import torch
 __all__ = [
     "local_mask", "alibi_bias", "attention_ref", "attention_lse_ref",
     "random_padding_mask", "unpad_input", "pad_input", "block_kvcache",
-    "parity_ok", "expand_kv",
+    "parity_ok", "expand_kv", "apply_rotary",
 ]
 
 
@@ -243,3 +249,25 @@ def parity_ok(out, out_ref, out_pt, mult: float = 2.0, atol: float = 0.0):
     err = (out.float() - out_ref.float()).abs().max().item()
     bound = mult * (out_pt.float() - out_ref.float()).abs().max().item() + atol
     return err <= bound, err, bound
+
+
+def apply_rotary(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                 seqlen_offsets: torch.Tensor, interleaved: bool = False) -> torch.Tensor:
+    """Rotary embedding of x [b, s, h, d] over its first 2 * cos.shape[1] features; token s of
+    batch b uses row seqlen_offsets[b] + s of cos/sin ([seqlen_ro, rotary_dim / 2]).  Computed
+    in fp32, returned in x's dtype (flash_attn.layers.rotary.apply_rotary_emb semantics)."""
+    b, s, h, d = x.shape
+    rd = 2 * cos.shape[1]
+    pos = seqlen_offsets.view(-1, 1).long().cpu() + torch.arange(s).view(1, -1)   # [b, s]
+    c = cos.float().cpu()[pos].unsqueeze(2)          # [b, s, 1, rd/2]
+    sn = sin.float().cpu()[pos].unsqueeze(2)
+    xf = x.float().cpu()
+    xr = xf[..., :rd]
+    if interleaved:
+        x1, x2 = xr[..., 0::2], xr[..., 1::2]
+        o1, o2 = x1 * c - x2 * sn, x1 * sn + x2 * c
+        out = torch.stack((o1, o2), dim=-1).reshape(b, s, h, rd)
+    else:
+        x1, x2 = xr[..., : rd // 2], xr[..., rd // 2:]
+        out = torch.cat((x1 * c - x2 * sn, x1 * sn + x2 * c), dim=-1)
+    return torch.cat((out, xf[..., rd:]), dim=-1).to(x.dtype)

@@ -396,3 +396,93 @@ def test_paged_fp8_capi(xfa):
     L.fmha_page_kvcache_fwd_ex(*args, 7, 1.0, 1.0, 0, st)
     assert L.fmha_last_status() != 0
     assert b"kv_dtype" in L.fmha_last_error()
+
+
+@pytest.mark.parametrize("paged", [True, False])
+@pytest.mark.parametrize("rotary_fraction", [0.0, 0.5, 1.0])
+@pytest.mark.parametrize("rotary_interleaved", [False, True])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("mha_type", ["mha", "gqa"])
+@pytest.mark.parametrize("seqlen_q,seqlen_k", [(1, 128), (3, 339), (64, 256)])
+def test_kvcache_append(xfa, paged, rotary_fraction, rotary_interleaved, causal, mha_type,
+                        seqlen_q, seqlen_k):
+    """Append new K/V (+ rotary) into the cache, then attend: the recipe of the reference's
+    test_flash_attn_kvcache with new_kv=True (test.py:1355-1594), whose rotary branch is
+    commented out there — rotary parity is pinned by oracle.apply_rotary only."""
+    if rotary_fraction == 0.0 and rotary_interleaved:
+        pytest.skip("interleaving is meaningless without rotary")
+    torch.manual_seed(0)
+    dtype = torch.bfloat16
+    b, h, d = 2, 6, 128
+    hk = h if mha_type == "mha" else 3
+    rotary_dim = int(rotary_fraction * d) // 16 * 16
+    seqlen_new = seqlen_q
+    q = torch.randn(b, seqlen_q, h, d, dtype=dtype)
+    k = torch.randn(b, seqlen_new, hk, d, dtype=dtype)
+    v = torch.randn(b, seqlen_new, hk, d, dtype=dtype)
+    page = 16
+    if paged:
+        kc, vc, table, kp, vp, nblk = orc.block_kvcache(seqlen_k, page, b, hk, d, dtype=dtype)
+    else:
+        kc = torch.randn(b, seqlen_k, hk, d, dtype=dtype)
+        vc = torch.randn(b, seqlen_k, hk, d, dtype=dtype)
+    hi = seqlen_k - (seqlen_q if causal and rotary_dim > 0 else seqlen_new) + 1
+    cache_seqlens = torch.randint(0, hi, (b,), dtype=torch.int32)
+    arange = torch.arange(seqlen_k).view(1, -1)
+    cs = cache_seqlens.view(-1, 1)
+    kpm = arange < cs + seqlen_new
+    if rotary_dim > 0:
+        angle = torch.rand(seqlen_k if not paged else nblk * page, rotary_dim // 2) * 2 * math.pi
+        cos, sin = torch.cos(angle).to(dtype), torch.sin(angle).to(dtype)
+        if causal:
+            q_ro = orc.apply_rotary(q, cos, sin, cache_seqlens, rotary_interleaved)
+        else:
+            q_ro = orc.apply_rotary(q.reshape(b, 1, seqlen_q * h, d), cos, sin, cache_seqlens,
+                                    rotary_interleaved).reshape(b, seqlen_q, h, d)
+        k_ro = orc.apply_rotary(k, cos, sin, cache_seqlens, rotary_interleaved)
+    else:
+        cos = sin = None
+        q_ro, k_ro = q, k
+    upd = (cs <= arange) & (arange < cs + seqlen_new)
+    k_ref, v_ref = kc.clone(), vc.clone()
+    k_ref[upd] = k_ro.reshape(-1, hk, d)
+    v_ref[upd] = v.reshape(-1, hk, d)
+    kd = (kp if paged else kc).clone().to(DEV)
+    vd = (vp if paged else vc).clone().to(DEV)
+    out = xfa.flash_attn_with_kvcache(
+        q.to(DEV), kd, vd, k.to(DEV), v.to(DEV),
+        rotary_cos=None if cos is None else cos.to(DEV),
+        rotary_sin=None if sin is None else sin.to(DEV),
+        cache_seqlens=cache_seqlens.to(DEV), block_table=table.to(DEV) if paged else None,
+        causal=causal, rotary_interleaved=rotary_interleaved)
+    torch.cuda.synchronize()
+    if paged:
+        nb = table.shape[1]
+        ksel = kd.cpu()[table.long().flatten()].reshape(b, nb * page, hk, d)[:, :seqlen_k]
+        vsel = vd.cpu()[table.long().flatten()].reshape(b, nb * page, hk, d)[:, :seqlen_k]
+    else:
+        ksel, vsel = kd.cpu(), vd.cpu()
+    assert torch.allclose(ksel.float(), k_ref.float(), rtol=1e-3, atol=1e-3)
+    assert torch.equal(vsel, v_ref)
+    r, _ = orc.attention_ref(q_ro, k_ref, v_ref, None, kpm, causal=causal)
+    pt, _ = orc.attention_ref(q_ro, k_ref, v_ref, None, kpm, causal=causal, upcast=False,
+                              reorder_ops=True)
+    _assert_parity(out, r, pt, mult=3.0, atol=1e-5, what="kvcache append")
+
+
+def test_kvcache_cache_batch_idx(xfa):
+    """Dense cache indexed through cache_batch_idx (batch b reads cache row idx[b])."""
+    torch.manual_seed(4)
+    b, bc, h, d, sk = 2, 5, 4, 64, 200
+    q = torch.randn(b, 1, h, d, dtype=torch.float16)
+    kc = torch.randn(bc, sk, h, d, dtype=torch.float16)
+    vc = torch.randn(bc, sk, h, d, dtype=torch.float16)
+    idx = torch.tensor([3, 1], dtype=torch.int32)
+    lens = torch.tensor([200, 57], dtype=torch.int32)
+    out = xfa.flash_attn_with_kvcache(q.to(DEV), kc.to(DEV), vc.to(DEV), cache_seqlens=lens.to(DEV),
+                                      cache_batch_idx=idx.to(DEV))
+    ks, vs = kc[idx.long()], vc[idx.long()]
+    kpm = torch.arange(sk).view(1, -1) < lens.view(-1, 1)
+    r, _ = orc.attention_ref(q, ks, vs, None, kpm)
+    pt, _ = orc.attention_ref(q, ks, vs, None, kpm, upcast=False, reorder_ops=True)
+    _assert_parity(out, r, pt, mult=3.0, atol=1e-5, what="cache_batch_idx")

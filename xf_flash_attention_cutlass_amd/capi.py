@@ -33,6 +33,8 @@ _SIGS = {
     "fmha_varlen_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                         i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp, vp, sz],
     "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32],
+    "fmha_kvcache_append": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, b_,
+                            b_, i32, i32, i32, i32, i32, b_, vp],
     "fmha_last_error": [],
     "fmha_last_status": [],
     "fmha_version": [],

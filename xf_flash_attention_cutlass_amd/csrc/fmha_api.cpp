@@ -367,6 +367,51 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
     }
 }
 
+void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const void* knew,
+                         const void* vnew, int32_t seqlen_new, const void* block_table,
+                         int32_t block_table_stride, int32_t page_block_size,
+                         const void* cache_seqlens, void* seqlens_out, const void* rotary_cos,
+                         const void* rotary_sin, int32_t rotary_dim, bool is_rotary_interleaved,
+                         bool q_rotary_per_token, int32_t batch_size, int32_t seqlen_q,
+                         int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                         bool is_fp16, hipStream_t stream) {
+    try {
+        clear_error();
+        REQUIRE(kcache && vcache && block_table && cache_seqlens,
+                "kcache, vcache, block_table and cache_seqlens must be given");
+        REQUIRE(seqlen_new >= 0, "seqlen_new must be >= 0");
+        REQUIRE(seqlen_new == 0 || (knew && vnew), "new K and V must both be given");
+        REQUIRE(batch_size > 0 && num_heads > 0 && num_heads_k > 0 && num_heads % num_heads_k == 0,
+                "invalid batch / head counts");
+        REQUIRE(head_size > 0 && head_size % 8 == 0 && head_size <= 256,
+                "head_size must be a multiple of 8 (<= 256) for the append pass");
+        REQUIRE(page_block_size > 0, "page_block_size must be positive");
+        REQUIRE(rotary_dim >= 0 && rotary_dim <= head_size && rotary_dim % 16 == 0,
+                "Only rotary dimensions divisible by 16 and <= headdim are supported");
+        REQUIRE(rotary_dim == 0 || (rotary_cos && rotary_sin && q && q_out),
+                "rotary needs cos, sin, q and q_out");
+        AppendParams p{};
+        p.q = q; p.q_out = q_out; p.kcache = kcache; p.vcache = vcache;
+        p.knew = knew; p.vnew = vnew;
+        p.block_table = (const int*)block_table; p.bt_stride = block_table_stride;
+        p.page = page_block_size;
+        p.cache_seqlens = (const int*)cache_seqlens; p.seqlens_out = (int*)seqlens_out;
+        p.cos = rotary_cos; p.sin = rotary_sin; p.rdim = rotary_dim;
+        p.interleaved = is_rotary_interleaved; p.q_per_token = q_rotary_per_token;
+        p.b = batch_size; p.sq = seqlen_q; p.h = num_heads; p.hk = num_heads_k; p.d = head_size;
+        p.snew = seqlen_new;
+        p.q_head = head_size; p.q_row = (int64_t)num_heads * head_size;
+        p.q_batch = (int64_t)seqlen_q * p.q_row;
+        p.kn_head = head_size; p.kn_row = (int64_t)num_heads_k * head_size;
+        p.kn_batch = (int64_t)seqlen_new * p.kn_row;
+        p.head_stride = head_size; p.row_stride = (int64_t)num_heads_k * head_size;
+        p.page_stride = (int64_t)page_block_size * p.row_stride;
+        hip_ok(launch_append(p, is_fp16, stream), "append launch");
+    } catch (...) {
+        fail(9, "internal error in fmha_kvcache_append");
+    }
+}
+
 void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void* /*k_ptr*/,
                            void* /*v_ptr*/, void* o_ptr, void* block_table_ptr,
                            void* cache_seqlens_k_ptr, const int32_t max_cache_seq_k,

@@ -36,6 +36,21 @@ hipError_t launch_bwd_hd64_f16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_bf16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_f16(const BwdParams& p, hipStream_t st);
 
+// KV-cache append (+ rotary) pass, fmha_append.hip
+struct AppendParams {
+    const void* q; void* q_out;
+    void* kcache; void* vcache;
+    const void* knew; const void* vnew;
+    const int* block_table; int bt_stride; int page;
+    const int* cache_seqlens; int* seqlens_out;
+    const void* cos; const void* sin; int rdim; int interleaved; int q_per_token;
+    int b, sq, h, hk, d, snew;
+    int64_t q_batch, q_row, q_head;          // elements (q and q_out share the layout)
+    int64_t kn_batch, kn_row, kn_head;       // elements (knew / vnew share the layout)
+    int64_t page_stride, row_stride, head_stride;   // cache strides (elements)
+};
+hipError_t launch_append(const AppendParams& p, bool fp16, hipStream_t st);
+
 inline int fwd_block_m() { return options().fwd_pp ? 256 : options().fwd_waves * 32; }
 inline int fwd_num_m_blocks(int seqlen_q, int group) {
     return (seqlen_q * group + fwd_block_m() - 1) / fwd_block_m();

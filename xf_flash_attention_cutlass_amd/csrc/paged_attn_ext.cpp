@@ -3,7 +3,9 @@
 // Mirrors the reference's export.cpp (module export.cpp:1757-1764): `fwd` (mha_fwd,
 // export.cpp:465-667), `varlen_fwd` (mha_varlen_fwd, :669-937), `fwd_kvcache`
 // (mha_fwd_kvcache, :1433-1754) with the same argument lists and return tuples, plus `bwd`
-// and `varlen_bwd`, which the reference has only as dead code (:939-1431).  Every op
+// and `varlen_bwd`, which the reference has only as dead code (:939-1431).  `fwd_kvcache`
+// also appends new K/V (with optional rotary) into the cache, which the reference validates
+// but never executes (export.cpp:1585-1669, csrc/paged_attn.cpp:513-525).  Every op
 // validates with TORCH_CHECK, allocates outputs, and calls the C ABI of
 // libpaged-attention.so (include/paged_attn.h); errors reported by the C ABI are re-raised
 // as RuntimeError.  Behaviour the reference gets wrong is fixed, not copied:
@@ -251,13 +253,10 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
                 c10::optional<at::Tensor>& block_table_, c10::optional<at::Tensor>& alibi_slopes_,
                 c10::optional<at::Tensor>& out_, const float softmax_scale, bool is_causal,
                 int window_size_left, int window_size_right, const float softcap,
-                bool /*is_rotary_interleaved*/, int num_splits) {
+                bool is_rotary_interleaved, int num_splits) {
     check_qkv_dtype(q, kcache, vcache);
-    TORCH_CHECK(!k_.has_value() && !v_.has_value(),
-                "appending new K/V to the cache is not supported by this build");
-    TORCH_CHECK(!rotary_cos_.has_value() && !rotary_sin_.has_value(),
-                "rotary embedding on append is not supported by this build");
-    TORCH_CHECK(!cache_batch_idx_.has_value(), "cache_batch_idx is not supported by this build");
+    const bool append = k_.has_value();
+    const bool local_or_causal = is_causal || window_size_left >= 0 || window_size_right >= 0;
     at::Tensor block_table;
     const bool paged_KV = block_table_.has_value();
     if (paged_KV) {
@@ -285,12 +284,25 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
     if (window_size_right >= seqlen_k) window_size_right = -1;
     CHECK_SHAPE(q, batch_size, seqlen_q, num_heads, head_size_og);
     if (!paged_KV) {
-        // Dense cache [batch, seqlen_k, hk, d]: one "page" per sequence (the reference's
-        // non-paged branch dereferences an undefined block_table, export.cpp:1711).
-        CHECK_SHAPE(kcache, batch_size, page_block_size, num_heads_k, head_size_og);
-        CHECK_SHAPE(vcache, batch_size, page_block_size, num_heads_k, head_size_og);
-        block_table = torch::arange(batch_size, q.options().dtype(torch::kInt32)).view({batch_size, 1});
+        // Dense cache [batch_cache, seqlen_k, hk, d]: one "page" per sequence (the reference's
+        // non-paged branch dereferences an undefined block_table, export.cpp:1711); the page of
+        // batch b is cache_batch_idx[b] when given, else b.
+        const int bc = kcache.size(0);
+        CHECK_SHAPE(kcache, bc, page_block_size, num_heads_k, head_size_og);
+        CHECK_SHAPE(vcache, bc, page_block_size, num_heads_k, head_size_og);
+        if (cache_batch_idx_.has_value()) {
+            auto idx = cache_batch_idx_.value();
+            CHECK_DEVICE(idx); CHECK_CONTIGUOUS(idx);
+            TORCH_CHECK(idx.scalar_type() == torch::kInt32, "cache_batch_idx must have dtype int32");
+            CHECK_SHAPE(idx, batch_size);
+            block_table = idx.view({batch_size, 1});
+        } else {
+            TORCH_CHECK(bc == batch_size, "k_cache batch must equal q batch without cache_batch_idx");
+            block_table = torch::arange(batch_size, q.options().dtype(torch::kInt32)).view({batch_size, 1});
+        }
     } else {
+        TORCH_CHECK(!cache_batch_idx_.has_value(),
+                    "cache_batch_idx cannot be combined with a paged KV cache");
         CHECK_SHAPE(kcache, num_blocks, page_block_size, num_heads_k, head_size_og);
         CHECK_SHAPE(vcache, num_blocks, page_block_size, num_heads_k, head_size_og);
         CHECK_SHAPE(block_table, batch_size, max_num_blocks_per_seq);
@@ -323,7 +335,57 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
     }
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
-    fmha_page_kvcache_fwd_ex(q_padded.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(),
+    at::Tensor q_attn = q_padded;
+    if (append) {
+        // write the new rows into the cache in place (+ rotary on k and q), then attend over the
+        // cache with the grown lengths (export.cpp:1585-1669 validation)
+        TORCH_CHECK(v_.has_value(), "If key is supplied, value must also be passed in");
+        TORCH_CHECK(seqlens.defined(), "If key is supplied, seqlens_k must also be passed in");
+        const at::Tensor& kn = k_.value();
+        const at::Tensor& vn = v_.value();
+        TORCH_CHECK(kn.dtype() == q.dtype(), "Key must have the same dtype as query");
+        TORCH_CHECK(vn.dtype() == q.dtype(), "Value must have the same dtype as query");
+        CHECK_DEVICE(kn); CHECK_DEVICE(vn); CHECK_CONTIGUOUS(kn); CHECK_CONTIGUOUS(vn);
+        const int seqlen_new = kn.size(1);
+        CHECK_SHAPE(kn, batch_size, seqlen_new, num_heads_k, head_size_og);
+        CHECK_SHAPE(vn, batch_size, seqlen_new, num_heads_k, head_size_og);
+        TORCH_CHECK(seqlen_q <= seqlen_k, "If key is supplied, it must have seqlen <= the seqlen of the KV cache");
+        TORCH_CHECK(head_size_og % 8 == 0 && kcache.is_contiguous() && vcache.is_contiguous(),
+                    "appending needs contiguous caches with head_size a multiple of 8 (updated in place)");
+        int rotary_dim = 0;
+        at::Tensor cos, sin, q_rot;
+        if (rotary_cos_.has_value()) {
+            TORCH_CHECK(rotary_sin_.has_value(), "If rotary cos is provided, rotary sin must also be provided");
+            cos = rotary_cos_.value();
+            sin = rotary_sin_.value();
+            CHECK_DEVICE(cos); CHECK_DEVICE(sin); CHECK_CONTIGUOUS(cos); CHECK_CONTIGUOUS(sin);
+            rotary_dim = cos.size(1) * 2;
+            TORCH_CHECK(rotary_dim <= head_size_og, "rotary_dim must be <= headdim");
+            TORCH_CHECK(rotary_dim % 16 == 0, "Only rotary dimensions divisible by 16 are currently supported");
+            TORCH_CHECK(cos.size(0) >= seqlen_k, "cos/sin seqlen must be at least the seqlen of KV cache");
+            CHECK_SHAPE(sin, cos.size(0), rotary_dim / 2);
+            TORCH_CHECK(cos.scalar_type() == q.scalar_type() && sin.scalar_type() == q.scalar_type(),
+                        "rotary_cos/sin must have the same dtype as query");
+            q_rot = torch::empty_like(q_padded);
+        }
+        auto seqlens_new = torch::empty_like(seqlens);
+        fmha_kvcache_append(q_padded.data_ptr(), q_rot.defined() ? q_rot.data_ptr() : nullptr,
+                            kc.data_ptr(), vc.data_ptr(), kn.data_ptr(), vn.data_ptr(), seqlen_new,
+                            block_table.data_ptr(), (int)block_table.stride(0), page_block_size,
+                            seqlens.data_ptr(), seqlens_new.data_ptr(),
+                            cos.defined() ? cos.data_ptr() : nullptr,
+                            sin.defined() ? sin.data_ptr() : nullptr, rotary_dim,
+                            is_rotary_interleaved, local_or_causal, batch_size, seqlen_q,
+                            num_heads, num_heads_k, head_size, q.dtype() == torch::kFloat16,
+                            cur_stream());
+        raise_if_failed("fwd_kvcache (append)");
+        seqlens = seqlens_new;
+        if (q_rot.defined()) q_attn = q_rot;
+    } else {
+        TORCH_CHECK(!rotary_cos_.has_value(),
+                    "If rotary cos/sin are provided, new key / value to be appended to KV cache must also be provided");
+    }
+    fmha_page_kvcache_fwd_ex(q_attn.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(),
                              softmax_lse.data_ptr(), block_table.data_ptr(),
                              (int)block_table.stride(0),
                              seqlens.defined() ? seqlens.data_ptr() : nullptr, seqlen_q, seqlen_k,

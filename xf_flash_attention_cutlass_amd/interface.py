@@ -127,7 +127,9 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
                             causal=False, window_size=(-1, -1), softcap=0.0,
                             rotary_interleaved=True, alibi_slopes=None, num_splits=0,
                             return_softmax_lse=False, k_scale=1.0, v_scale=1.0):
-    """Decode / chunked prefill against a (paged) KV cache (test.py:189-245).
+    """Decode / chunked prefill against a (paged) KV cache (test.py:189-245).  With k/v the new
+    rows are first written into the cache in place at cache_seqlens (rotary_cos/sin: rotary
+    embedding on k and q, interleaved = GPT-J pairs), then attended over.
 
     Extension: a `torch.float8_e4m3fn` paged cache is read natively (dequantised in-kernel as
     fp8 * k_scale / v_scale); it requires `block_table` and `cache_seqlens`."""
@@ -154,7 +156,7 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
                                               int(window_size[1]), num_splits)
         return (out, lse) if return_softmax_lse else out
     if cache_seqlens is not None and isinstance(cache_seqlens, int):
-        cache_seqlens = torch.full((k_cache.shape[0],), cache_seqlens, dtype=torch.int32,
+        cache_seqlens = torch.full((q.shape[0],), cache_seqlens, dtype=torch.int32,
                                    device=k_cache.device)
         cache_seqlens = _maybe_contiguous(cache_seqlens)
     cache_batch_idx = _maybe_contiguous(cache_batch_idx)
