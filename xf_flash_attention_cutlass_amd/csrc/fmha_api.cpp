@@ -200,6 +200,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.store8 = options().fwd_store8;
     p.pipe = options().fwd_pipe;
     p.dbg = options().fwd_dbg;
+    p.max_slack = (float)options().fwd_slack;
     options().num_cus = num_cus();
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
@@ -226,6 +227,12 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_store8")) { options().fwd_store8 = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
     if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
+    if (!strcmp(name, "fwd_slack")) {
+        if (value < 0 || value > 16) { fail(1, "fwd_slack must be in [0, 16]"); return -1; }
+        options().fwd_slack = value;
+        return 0;
+    }
+    if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
     fail(1, "unknown option '%s'", name);

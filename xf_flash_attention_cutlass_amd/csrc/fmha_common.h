@@ -81,6 +81,8 @@ struct FwdParams {
     int n_mblocks;             // row blocks per (b, kv head) (persistent mode)
     int pipe;                  // 1: software-pipelined loop over the unmasked key tiles
     int dbg;                   // timing experiments only (results invalid when set)
+    float max_slack;           // log2 units the running max may lag the true max before the
+                               // O / l rescale (deferred rescale; 0 = rescale on every rise)
     int decode;                // 1: run fmha_decode_kernel (split-KV decode)
 };
 

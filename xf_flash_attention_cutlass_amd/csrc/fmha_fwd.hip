@@ -64,7 +64,10 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     if (!PP && options().fwd_persistent > 0) {
         const int items = p.b * p.hk * n_mb;
         const int slots = options().num_cus * options().fwd_persistent;
-        if (items > slots) { pp.persistent = 1; grid = dim3(slots, 1, grid.z); }
+        if (items > slots) {
+            pp.persistent = (options().fwd_order == 1 && slots % 8 == 0) ? 2 : 1;
+            grid = dim3(slots, 1, grid.z);
+        }
     }
     const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(4 * 2 * kBlockN * HD * 2);
     void (*kern)(const FwdParams);

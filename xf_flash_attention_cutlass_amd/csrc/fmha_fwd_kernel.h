@@ -125,7 +125,9 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         for (int s = 0; s < NS; ++s) {
             const int d0 = 16 * s + 8 * hh;
             const int off = (row_ok && d0 < p.d) ? qrow_off + d0 * 2 : kOOB;
-            qf[s] = __builtin_bit_cast(V8, buf_load16(qr, off));
+            if (p.dbg & 8) qf[s] = __builtin_bit_cast(V8, u32x4{(uint32_t)lane, 0u, 0u, 0u});  // timing only
+            else if (p.dbg & 32) qf[s] = __builtin_bit_cast(V8, buf_load16(qr, (tid * NS + s) * 16));
+            else qf[s] = __builtin_bit_cast(V8, buf_load16(qr, off));
         }
     }
 
@@ -251,9 +253,13 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     };
     // Exact lazy rescale: only when some row of this wave raised its running max (the O^T
     // rescale is a 64-register VALU pass; after the first tiles it is rare).
+    // Deferred rescale: the running max m_run (the exp reference) only moves once some row's
+    // true max exceeds it by more than max_slack (log2 units), so P = exp2(S c - m_run c) stays
+    // below 2^max_slack; O, l and the LSE are all relative to the same m_run, so the result is
+    // unchanged up to rounding (the relative rounding of P in T does not depend on the scale).
     auto raise_max = [&](const float mx) {
         const float m_new = fmaxf(m_run, mx);
-        if (__any(m_new > m_run)) {
+        if (__any(m_new * c > m_run * c + p.max_slack)) {
             const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
             const float alpha = fast_exp2(m_run * c - mref);
             l_run *= alpha;
@@ -433,23 +439,28 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // rows cannot see such a tile computes zeros for it instead of branching out of the
     // interleaved schedule).
     auto pipe_range = [&](const int lo, const int hm, const int hi) {
-        dma_tile(lo, 0);
-        dma_tile(lo + 1, 1);
         const bool third = lo + 2 < hi;
-        if (third) dma_tile(lo + 2, 2);
+        if (!(p.dbg & 16)) {                       // (dbg 16: timing only, no prologue loads)
+            dma_tile(lo, 0);
+            dma_tile(lo + 1, 1);
+            if (third) dma_tile(lo + 2, 2);
+        }
         publish(third);
-        f32x16 st[2];
-        qk(0, st);
-        transform_part(st, lo * kBlockN, lo >= hm, 0, 32);
-        raise_max(row_max(st));
+        // scores ping-pong between sa and sb from step to step (st: this tile, sn: the next),
+        // so the QK^T accumulators never need a register copy onto a loop-carried value
+        f32x16 sa[2], sb[2];
+        qk(0, sa);
+        transform_part(sa, lo * kBlockN, lo >= hm, 0, 32);
+        raise_max(row_max(sa));
         const int nsteps = hi - lo - 1;
-        auto step = [&](auto KB, auto VB, auto WB, const int j) {
+        auto step = [&](auto KB, auto VB, auto WB, const int j, f32x16 (&st)[2], f32x16 (&sn)[2]) {
             constexpr int ks = decltype(KB)::value, vs = decltype(VB)::value, wb = decltype(WB)::value;
             const bool issue = j + 3 < hi;
             if (issue) dma_tile(j + 3, wb);
             if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             // phase a: S_{j+1} = K_{j+1} Q^T on the MFMA pipe, P_j = exp(S_j) on the VALU
-            f32x16 sn[2] = {f32x16{}, f32x16{}};
+            sn[0] = f32x16{};
+            sn[1] = f32x16{};
             V8 pb[4];
             const f2 m2 = exp_ref();
             float rs[2] = {0.f, 0.f};
@@ -507,8 +518,6 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 for (int v = 1; v < 32; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
             }
             raise_max(wave_max_halves(mx));
-            st[0] = sn[0];
-            st[1] = sn[1];
             publish(issue);                       // tile j+2 landed everywhere
         };
         typedef std::integral_constant<int, 0> I0;
@@ -518,18 +527,19 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         // step r (tile j = lo + r) reads K of j+1 from buffer (r+1)%4 and V of j from r%4
         int r = 0;
         while (r < nsteps) {
-            step(I1{}, I0{}, I3{}, lo + r);
+            step(I1{}, I0{}, I3{}, lo + r, sa, sb);
             if (++r >= nsteps) break;
-            step(I2{}, I1{}, I0{}, lo + r);
+            step(I2{}, I1{}, I0{}, lo + r, sb, sa);
             if (++r >= nsteps) break;
-            step(I3{}, I2{}, I1{}, lo + r);
+            step(I3{}, I2{}, I1{}, lo + r, sa, sb);
             if (++r >= nsteps) break;
-            step(I0{}, I3{}, I2{}, lo + r);
+            step(I0{}, I3{}, I2{}, lo + r, sb, sa);
             ++r;
         }
         // drain: the last tile's softmax and PV
         V8 pb[4];
-        exp_tile(st, pb);
+        if (nsteps & 1) exp_tile(sb, pb);
+        else exp_tile(sa, pb);
         pv(nsteps & 3, pb);
         __syncthreads();
     };
@@ -594,7 +604,20 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
     const int g = gridDim.x;
     for (int k = 0;; ++k) {        // one call site: the item body is inlined once
         int bh, m_block;
-        if (p.persistent) {
+        if (p.persistent == 2) {
+            // XCD-grouped pairs: pair i of (b, kv head) = row blocks (n-1-i, i), equal causal
+            // work; consecutive pairs of one (b, kv head) run at the same time on the CUs of
+            // one XCD (workgroup bid sits on XCD bid % 8), so they share that XCD's L2 for K/V
+            const int nm = p.n_mblocks, npair = (nm + 1) >> 1;
+            const int bid = (int)blockIdx.x;
+            const int v = (bid & 7) * (g >> 3) + (bid >> 3);
+            const int q = (k >> 1) * g + v;
+            if (q >= nbh * npair) break;
+            bh = q / npair;
+            const int i = q - bh * npair;
+            m_block = (k & 1) ? i : nm - 1 - i;
+            if ((k & 1) && i == nm - 1 - i) continue;   // odd count: the middle block is alone
+        } else if (p.persistent) {
             const int lin = k * g + ((k & 1) ? g - 1 - (int)blockIdx.x : (int)blockIdx.x);
             if (lin >= nbh * p.n_mblocks) break;
             bh = lin % nbh;
