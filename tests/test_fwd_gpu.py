@@ -486,3 +486,46 @@ def test_kvcache_cache_batch_idx(xfa):
     r, _ = orc.attention_ref(q, ks, vs, None, kpm)
     pt, _ = orc.attention_ref(q, ks, vs, None, kpm, upcast=False, reorder_ops=True)
     _assert_parity(out, r, pt, mult=3.0, atol=1e-5, what="cache_batch_idx")
+
+
+# ------------------------------------------------------------ persistent forward: item order ---
+@pytest.mark.parametrize("cfg", [
+    dict(b=2, h=32, hk=8, s=2048, d=128, causal=True),
+    dict(b=2, h=32, hk=32, s=2048, d=64, causal=True),
+    dict(b=2, h=16, hk=16, s=3000, d=128, causal=False),
+    dict(b=1, h=32, hk=4, s=4093, d=96, causal=True),
+    dict(b=2, h=16, hk=16, s=2048, d=128, causal=False, window=(300, 0)),
+    dict(b=2, h=16, hk=16, s=2048, d=128, causal=False, window=(-1, 100)),
+])
+def test_fwd_persistent_order_bitexact(xfa, cfg):
+    """Persistent grid (items > resident workgroups): the XCD-grouped item order changes neither
+    bits of O nor of the LSE (an item's arithmetic does not depend on where it runs), and the
+    result stays within the reference rule of the oracle."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(11)
+    b, h, hk, s, d = cfg["b"], cfg["h"], cfg["hk"], cfg["s"], cfg["d"]
+    q = torch.randn(b, s, h, d, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(b, s, hk, d, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(b, s, hk, d, device=DEV, dtype=torch.bfloat16)
+    window = cfg.get("window", (-1, -1))
+    outs = []
+    try:
+        for order in (0, 1):
+            assert L.fmha_set_option(b"fwd_order", order) == 0
+            o, lse = xfa.flash_attn_func(q, k, v, causal=cfg["causal"], window_size=window,
+                                         return_attn_probs=True)[:2]
+            outs.append((o.clone(), lse.clone()))
+    finally:
+        L.fmha_set_option(b"fwd_order", 1)
+    for o, lse in outs[1:]:
+        assert torch.equal(o, outs[0][0])
+        assert torch.equal(lse, outs[0][1])
+    if True:                                  # oracle on the first 4 query heads of batch 0
+        qs, ks, vs = q[:1, :, :4], k[:1, :, :max(1, 4 * hk // h)], v[:1, :, :max(1, 4 * hk // h)]
+        r, _ = orc.attention_ref(qs.float(), ks.float(), vs.float(), causal=cfg["causal"],
+                                 window_size=window)
+        pt, _ = orc.attention_ref(qs, ks, vs, causal=cfg["causal"], window_size=window,
+                                  upcast=False, reorder_ops=True)
+        _assert_parity(outs[-1][0][:1, :, :4].float().cpu(), r.cpu(), pt.float().cpu(),
+                       what=str(cfg))

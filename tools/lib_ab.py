@@ -1,0 +1,102 @@
+"""In-process A/B timing of DIFFERENT BUILDS of libpaged-attention.so through the C ABI
+(interleaved rounds on one device, so box-to-box clock differences cancel;
+cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/lib_ab.py libA.so libB.so [--mode fwd|bwd] [--rounds 5] [--noncausal]
+
+Each path is loaded as its own ctypes library (copy it under a distinct file name first:
+the dynamic loader dedups by soname/path).  Options (--opt name=value) apply to every build.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd"])
+    ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--b", type=int, default=4)
+    ap.add_argument("--h", type=int, default=32)
+    ap.add_argument("--hk", type=int, default=0)
+    ap.add_argument("--s", type=int, default=4096)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--noncausal", action="store_true")
+    a = ap.parse_args()
+
+    from xf_flash_attention_cutlass_amd import capi
+    libs = [capi.load(p) for p in a.libs]
+    for lib in libs:
+        for spec in a.opt:
+            name, val = spec.split("=")
+            assert lib.fmha_set_option(name.encode(), int(val)) == 0, lib.fmha_last_error()
+    hk = a.hk or a.h
+    causal = not a.noncausal
+    dt = torch.bfloat16
+    q = torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=dt)
+    k = torch.randn(a.b, a.s, hk, a.d, device="cuda", dtype=dt)
+    v = torch.randn(a.b, a.s, hk, a.d, device="cuda", dtype=dt)
+    o = torch.empty_like(q)
+    do = torch.randn_like(q)
+    lse = torch.empty(a.b, a.h, a.s, device="cuda", dtype=torch.float32)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    sc = a.d ** -0.5
+    wr = 0 if causal else -1
+    stream = torch.cuda.current_stream().cuda_stream
+    P = lambda t: t.data_ptr()  # noqa: E731
+
+    def run(lib):
+        lib.fmha_fwd(P(q), P(k), P(v), P(o), None, a.s, a.s, a.b, a.h, hk, a.d, 0.0, stream, None,
+                     sc, None, P(lse), -1, wr, 0.0, False, False, 0)
+        if a.mode == "bwd":
+            lib.fmha_bwd(P(do), P(q), P(k), P(v), P(o), P(lse), P(dq), P(dk), P(dv), None, None,
+                         a.s, a.s, a.b, a.h, hk, a.d, 0.0, sc, -1, wr, 0.0, False, False, stream,
+                         None, 0)
+
+    fl = 4.0 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0) * (3.5 if a.mode == "bwd" else 1.0)
+    for lib in libs:
+        for _ in range(3):
+            run(lib)
+    torch.cuda.synchronize()
+    # ~1 s clock-ramp prewarm (bench.py does the same)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    n = 0
+    while True:
+        run(libs[0])
+        n += 1
+        if n % 20 == 0:
+            e1.record()
+            torch.cuda.synchronize()
+            if e0.elapsed_time(e1) > 1000:
+                break
+    times = {i: [] for i in range(len(libs))}
+    for _ in range(a.rounds):
+        for i, lib in enumerate(libs):
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(a.iters):
+                run(lib)
+            s1.record()
+            torch.cuda.synchronize()
+            times[i].append(s0.elapsed_time(s1) / a.iters)
+    for i, p in enumerate(a.libs):
+        med = statistics.median(times[i])
+        print(f"{a.mode} {os.path.basename(p)}: median {med:.4f} ms  min {min(times[i]):.4f}"
+              f"  -> {fl / med / 1e9:.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()

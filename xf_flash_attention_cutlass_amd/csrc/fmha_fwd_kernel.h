@@ -120,14 +120,16 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         const T* qseq = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch + (int64_t)q_off * p.q_row;
         const uint32_t qbytes = (uint32_t)(((int64_t)(sq - 1) * p.q_row + (int64_t)(p.h - 1) * p.q_head + p.d) * 2);
         const __amdgpu_buffer_rsrc_t qr = make_rsrc(qseq, qbytes);
-        const int qrow_off = (int)(((int64_t)pos * p.q_row + (int64_t)head * p.q_head) * 2);
+        // column part as an immediate offset; the asm keeps per-column offsets from being
+        // hoisted out of the persistent item loop (and spilled)
+        int hh_q = hh;
+        asm volatile("" : "+v"(hh_q));
+        const int qrow_off = row_ok ? (int)(((int64_t)pos * p.q_row + (int64_t)head * p.q_head) * 2) + 16 * hh_q : kOOB;
+        const bool full_d = p.d == HD;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const int d0 = 16 * s + 8 * hh;
-            const int off = (row_ok && d0 < p.d) ? qrow_off + d0 * 2 : kOOB;
-            if (p.dbg & 8) qf[s] = __builtin_bit_cast(V8, u32x4{(uint32_t)lane, 0u, 0u, 0u});  // timing only
-            else if (p.dbg & 32) qf[s] = __builtin_bit_cast(V8, buf_load16(qr, (tid * NS + s) * 16));
-            else qf[s] = __builtin_bit_cast(V8, buf_load16(qr, off));
+            const int off = (full_d || 16 * s + 8 * hh_q < p.d) ? qrow_off : kOOB;
+            qf[s] = __builtin_bit_cast(V8, buf_load16(qr, off + 32 * s));
         }
     }
 
@@ -251,8 +253,6 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             if (need_mask && (key >= my_lr || key < my_ll)) st[kt][r] = -INFINITY;
         }
     };
-    // Exact lazy rescale: only when some row of this wave raised its running max (the O^T
-    // rescale is a 64-register VALU pass; after the first tiles it is rare).
     // Deferred rescale: the running max m_run (the exp reference) only moves once some row's
     // true max exceeds it by more than max_slack (log2 units), so P = exp2(S c - m_run c) stays
     // below 2^max_slack; O, l and the LSE are all relative to the same m_run, so the result is
@@ -440,11 +440,9 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // interleaved schedule).
     auto pipe_range = [&](const int lo, const int hm, const int hi) {
         const bool third = lo + 2 < hi;
-        if (!(p.dbg & 16)) {                       // (dbg 16: timing only, no prologue loads)
-            dma_tile(lo, 0);
-            dma_tile(lo + 1, 1);
-            if (third) dma_tile(lo + 2, 2);
-        }
+        dma_tile(lo, 0);
+        dma_tile(lo + 1, 1);
+        if (third) dma_tile(lo + 2, 2);
         publish(third);
         // scores ping-pong between sa and sb from step to step (st: this tile, sn: the next),
         // so the QK^T accumulators never need a register copy onto a loop-carried value
