@@ -24,8 +24,9 @@ _EXT = os.path.join(_HERE, "lib", "paged_attn" + (sysconfig.get_config_var("EXT_
 
 def _load_paged_attn():
     if not os.path.exists(_EXT):
-        raise ImportError(f"native module {_EXT} is missing: run `python -m "
-                          "xf_flash_attention_cutlass_amd.build` (no fallback exists)")
+        raise ImportError(f"native module {_EXT} is missing: run `python "
+                          "xf_flash_attention_cutlass_amd/build.py` or "
+                          "`python __graft_entry__.py build` (no fallback exists)")
     spec = importlib.util.spec_from_file_location("paged_attn", _EXT)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)

@@ -7,7 +7,7 @@ Produces
   xf_flash_attention_cutlass_amd/lib/paged_attn*.so          — the pybind/ATen module
       `paged_attn` (export.cpp equivalent), linked against libpaged-attention.so.
 
-Usage: python -m xf_flash_attention_cutlass_amd.build [--no-ext] [-j N] [--force]
+Usage: python xf_flash_attention_cutlass_amd/build.py [--no-ext] [-j N] [--force]
 """
 from __future__ import annotations
 

@@ -49,8 +49,8 @@ EXPORTED = tuple(_SIGS)
 
 def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
-        raise ImportError(f"native library {path} is missing: run `python -m "
-                          "xf_flash_attention_cutlass_amd.build` (no CPU fallback exists)")
+        raise ImportError(f"native library {path} is missing: run `python "
+                          "xf_flash_attention_cutlass_amd/build.py` (no CPU fallback exists)")
     lib = C.CDLL(path)
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
