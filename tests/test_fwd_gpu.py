@@ -328,9 +328,11 @@ def test_paged_fp8_generic_staging_bitexact(xfa):
                                        (1, 6, 6, 64), (3, 12, 1, 128)])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
+@pytest.mark.parametrize("tile16", [0, 1])
+def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype, tile16):
     """Decode shapes (sq * H/Hk <= 32) through mha_fwd (dense K/V) and through the paged cache,
-    against the oracle; the decode and general kernels agree to rounding."""
+    against the oracle; the decode and general kernels agree to rounding.  tile16 = 1 runs the
+    16x16x32 decode tile for groups of <= 16 query rows (option fwd_decode16)."""
     from xf_flash_attention_cutlass_amd import capi
     L = capi.lib()
     torch.manual_seed(5)
@@ -338,7 +340,11 @@ def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
     q = torch.randn(b, sq, h, d, dtype=dtype)
     k = torch.randn(b, sk, hk, d, dtype=dtype)
     v = torch.randn(b, sk, hk, d, dtype=dtype)
-    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
+    assert L.fmha_set_option(b"fwd_decode16", tile16) == 0
+    try:
+        out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
+    finally:
+        L.fmha_set_option(b"fwd_decode16", 0)
     r, _ = orc.attention_ref(q, k, v, causal=causal)
     pt, _ = orc.attention_ref(q, k, v, causal=causal, upcast=False, reorder_ops=True)
     _assert_parity(out, r, pt, what="decode dense")

@@ -235,6 +235,7 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_decode16")) { options().fwd_decode16 = value ? 1 : 0; return 0; }
     fail(1, "unknown option '%s'", name);
     return -1;
 }

@@ -8,7 +8,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace xfa {
+
+// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
 
 // ------------------------------------------------------------------ vector types --
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -19,7 +19,13 @@
 //  * a ring of raw K/V registers keeps the next tiles' loads in flight across the compute of
 //    the current tile (two tiles for fp8, one for 16-bit caches): a slot is refilled with the
 //    tile RING ahead as soon as its raw bytes are converted;
-//  * partial (O, LSE) per wave go to the split scratch; fmha_combine_kernel merges them.
+//  * partial (O, LSE) per wave go to the split scratch; fmha_combine_kernel merges them;
+//  * MR = 16 (GQA groups of <= 16 query rows, the common decode shape): S^T and O^T on
+//    v_mfma_f32_16x16x32 — half the MFMA cycles and half the softmax lanes of the 32-row tile,
+//    and the freed registers deepen the load ring (3 fp8 tiles in flight instead of 2).
+//    Lane l holds query row l % 16 and, of each 16-key block, keys 4 (l / 16) .. +3; the two
+//    blocks' P values are directly the B operand of the PV product with its k index permuted
+//    to key(8g + i) = i < 4 ? 4g + i : 16 + 4g + (i - 4), the same permutation applied to V^T.
 #pragma once
 
 #include "fmha_common.h"
@@ -46,24 +52,51 @@ template <> struct FP8Cvt<_Float16> {
     }
 };
 
-template <int HD, typename T, bool KV8>
+template <typename T> __device__ __forceinline__ f32x4 dec_mfma16(const typename DT<T>::v8& a,
+                                                                const typename DT<T>::v8& b, const f32x4& c);
+template <> __device__ __forceinline__ f32x4 dec_mfma16<__bf16>(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ f32x4 dec_mfma16<_Float16>(const f16x8& a, const f16x8& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// reductions over the four 16-lane groups that hold one query row (MR = 16)
+__device__ __forceinline__ float quad_max16(float x) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float quad_sum16(float x) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+template <int HD, typename T, bool KV8, int MR>
 __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const FwdParams p) {
     using V8 = typename DT<T>::v8;
-    constexpr int NS = HD / 16;                  // k-steps of S^T = K Q^T
-    constexpr int ND = HD / 32;                  // 32-wide d tiles of O^T
+    static_assert(MR == 16 || MR == 32, "MFMA rows");
+    constexpr int NS = MR == 32 ? HD / 16 : HD / 32;   // k-steps of S^T = K Q^T
+    constexpr int ND = HD / MR;                  // MR-wide d tiles of O^T
+    constexpr int NA = MR == 32 ? 16 : 4;        // accumulator registers per MR x MR tile
+    typedef float __attribute__((ext_vector_type(NA))) accv;
     constexpr int ESZ = KV8 ? 1 : 2;
     constexpr int CPR = HD * ESZ / 16;           // 16-byte chunks per K (V) row
     constexpr int RPI = 64 / CPR;                // rows per load instruction
     constexpr int NLD = kDecKeys / RPI;          // load instructions per lane per K (V) tile
-    constexpr int RING = KV8 ? 2 : 1;            // tiles in flight beyond the current one
+    // tiles in flight beyond the current one (bounded by the 256-VGPR budget of two waves
+    // per SIMD; the 16-row tile frees the registers for one more fp8 tile)
+    constexpr int RING = KV8 ? (MR == 16 ? 3 : 2) : 1;
     constexpr int SLICE = kDecKeys * HD * 2;     // LDS bytes of one wave's K (or V) image
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31;
-    const int hh = lane >> 5;
+    const int lr = lane & (MR - 1);               // query row (MFMA column) of this lane
+    const int hh = lane / MR;                     // key sub-block (0..64/MR-1) of this lane
     const int bh = blockIdx.x;
     const int bidx = bh / p.hk;
     const int hk_i = bh - bidx * p.hk;
@@ -71,7 +104,7 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     char* vsl = smem + wave * 2 * SLICE;         // this wave's V image; K image follows
 
     const int sq = p.seqlen_q;
-    const int sk = p.seqused_k ? p.seqused_k[bidx] : p.seqlen_k;
+    const int sk = __builtin_amdgcn_readfirstlane(p.seqused_k ? p.seqused_k[bidx] : p.seqlen_k);
     const int G = p.group;
     const int rows = sq * G;
     const int diag = sk - sq;
@@ -95,67 +128,83 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     const int t_lo = min(t_end, t_first + split * per);
     const int t_hi = min(t_end, t_lo + per);
 
-    // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][16s + 8hh .. +7]
+    // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[row][KS s + 8hh .. +7]
+    // (KS = the k depth of one MFMA: 16 for 32x32x16, 32 for 16x16x32)
+    constexpr int KS = MR == 32 ? 16 : 32;
     V8 qf[NS];
     {
         const T* qrow = reinterpret_cast<const T*>(p.q) + (int64_t)bidx * p.q_batch +
                         (int64_t)pos * p.q_row + (int64_t)head * p.q_head + 8 * hh;
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-            qf[s] = row_ok ? *reinterpret_cast<const V8*>(qrow + 16 * s) : V8{};
+            qf[s] = row_ok ? *reinterpret_cast<const V8*>(qrow + KS * s) : V8{};
     }
 
     // ---- K/V loads, coalesced: instruction i, lane l -> tile row RPI*i + l / CPR, 16-byte
-    // chunk l % CPR of that row (consecutive lanes read consecutive bytes of one row)
+    // chunk l % CPR of that row (consecutive lanes read consecutive bytes of one row).
+    // Addressing is scalar: one load instruction covers RPI <= 8 rows, which never straddle a
+    // page (pages are multiples of 16 rows, host-checked), so its page and row are wave-uniform
+    // and go into a buffer descriptor and soffset; the per-lane part (row in the group, chunk)
+    // is a loop-invariant voffset.  (Per-lane 64-bit paged address arithmetic — a division by
+    // the page size per row — was the decode kernel's largest instruction cost.)
     const bool paged = p.block_table != nullptr;
     const int lrow = lane / CPR, lch = lane % CPR;
-    const char* kbase = reinterpret_cast<const char*>(p.k) + (int64_t)hk_i * p.k_head * ESZ + 16 * lch;
-    const char* vbase = reinterpret_cast<const char*>(p.v) + (int64_t)hk_i * p.v_head * ESZ + 16 * lch;
+    const int lane_k = lrow * (int)p.k_row * ESZ + 16 * lch;
+    const int lane_v = lrow * (int)p.v_row * ESZ + 16 * lch;
+    const char* kpool = reinterpret_cast<const char*>(p.k) + (int64_t)hk_i * p.k_head * ESZ;
+    const char* vpool = reinterpret_cast<const char*>(p.v) + (int64_t)hk_i * p.v_head * ESZ;
     if (!paged) {
-        kbase += (int64_t)bidx * p.k_batch * ESZ;
-        vbase += (int64_t)bidx * p.v_batch * ESZ;
+        kpool += (int64_t)bidx * p.k_batch * ESZ;
+        vpool += (int64_t)bidx * p.v_batch * ESZ;
     }
+    const int krow_b = (int)p.k_row * ESZ, vrow_b = (int)p.v_row * ESZ;
     // Page-table entries are wave-uniform per (tile, page): a 32-key tile spans at most two
-    // pages when page_size % 16 == 0 (the host guarantees it), so they are scalar loads through
-    // the constant address space (lgkm-counted: they never make the vector-load ring drain),
-    // fetched one tile early.
+    // pages, so they are scalar loads through the constant address space (lgkm-counted: they
+    // never make the vector-load ring drain), fetched one tile early, together with the row of
+    // the tile start inside its first page.
     typedef __attribute__((address_space(4))) const int cint;
     cint* btab = paged ? (cint*)(p.block_table + (int64_t)bidx * p.bt_stride) : nullptr;
-    int pg_next[2] = {0, 0};
-    auto fetch_pages = [&](const int t, int (&pg)[2]) {
+    int pg_next[3] = {0, 0, 0};
+    auto fetch_pages = [&](const int t, int (&pg)[3]) __attribute__((always_inline)) {
         if (!paged) return;
         const int last = (sk - 1) / p.page_size;
         const int pi0 = __builtin_amdgcn_readfirstlane(min((t * kDecKeys) / p.page_size, last));
         pg[0] = btab[pi0];
         pg[1] = btab[min(pi0 + 1, last)];
+        pg[2] = t * kDecKeys - pi0 * p.page_size;    // may exceed the page past the last row
     };
+    const uint32_t page_k = (uint32_t)(p.page_size * krow_b), page_v = (uint32_t)(p.page_size * vrow_b);
+    const __amdgpu_buffer_rsrc_t kseq_rs =
+        make_rsrc(kpool, paged ? 0u : (uint32_t)min((int64_t)sk * krow_b, (int64_t)0xFFFFFFFF));
+    const __amdgpu_buffer_rsrc_t vseq_rs =
+        make_rsrc(vpool, paged ? 0u : (uint32_t)min((int64_t)sk * vrow_b, (int64_t)0xFFFFFFFF));
 
     u32x4 kraw[RING][NLD], vraw[RING][NLD];
-    auto issue = [&](const int t, const int (&pg)[2], u32x4 (&kr)[NLD], u32x4 (&vr)[NLD]) {
-        int64_t ko[NLD], vo[NLD];
+    auto issue = [&](const int t, const int (&pg)[3], u32x4 (&kr)[NLD], u32x4 (&vr)[NLD]) __attribute__((always_inline)) {
         if (paged) {
-            const int pi0 = (t * kDecKeys) / p.page_size;
+            // past the last key the page index is clamped, so the rows of a group that wraps
+            // there re-read rows of the last page: keys >= seqlen, masked in registers
 #pragma unroll
             for (int i = 0; i < NLD; ++i) {
-                const int n = min(t * kDecKeys + RPI * i + lrow, sk - 1);   // clamped rows
-                const int pi = n / p.page_size;
-                const int pgl = pi == pi0 ? pg[0] : pg[1];
-                const int pr = n - pi * p.page_size;
-                ko[i] = ((int64_t)pgl * p.k_batch + (int64_t)pr * p.k_row) * ESZ;
-                vo[i] = ((int64_t)pgl * p.v_batch + (int64_t)pr * p.v_row) * ESZ;
+                // (readfirstlane: the divergence analysis loses the uniformity of the page
+                // entries, and a descriptor it believes divergent becomes a waterfall loop)
+                int x = __builtin_amdgcn_readfirstlane(pg[2] + RPI * i);
+                const bool nxt = x >= p.page_size;
+                const int page = __builtin_amdgcn_readfirstlane(nxt ? pg[1] : pg[0]);
+                x = nxt ? x - p.page_size : x;
+                const __amdgpu_buffer_rsrc_t krs = make_rsrc(kpool + (int64_t)page * p.k_batch * ESZ, page_k);
+                const __amdgpu_buffer_rsrc_t vrs = make_rsrc(vpool + (int64_t)page * p.v_batch * ESZ, page_v);
+                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_k, x * krow_b, 0);
+                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_v, x * vrow_b, 0);
             }
         } else {
+            // rows >= sk fall outside the sequence descriptor and read as zeros
 #pragma unroll
             for (int i = 0; i < NLD; ++i) {
-                const int n = min(t * kDecKeys + RPI * i + lrow, sk - 1);
-                ko[i] = (int64_t)n * p.k_row * ESZ;
-                vo[i] = (int64_t)n * p.v_row * ESZ;
+                const int n = t * kDecKeys + RPI * i;
+                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(kseq_rs, lane_k, n * krow_b, 0);
+                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vseq_rs, lane_v, n * vrow_b, 0);
             }
-        }
-#pragma unroll
-        for (int i = 0; i < NLD; ++i) {
-            kr[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(kbase + ko[i]));
-            vr[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vbase + vo[i]));
         }
     };
 
@@ -168,30 +217,40 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     for (int i = 0; i < NLD; ++i)
 #pragma unroll
         for (int h2 = 0; h2 < 3 - ESZ; ++h2) kw[i][h2] = lds_off<HD>(RPI * i + lrow, (3 - ESZ) * lch + h2);
+    // K operand (A of S^T) of k-step s: row lr (key), 16-byte chunk s KS/8 + hh; the second
+    // 16-key block (MR = 16) is 16 rows on, same swizzle (the swizzle has period 16)
     int koff[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) koff[s] = lds_off<HD>(lr, 2 * s + hh);
+    for (int s = 0; s < NS; ++s) koff[s] = lds_off<HD>(lr, (KS / 8) * s + hh);
+    // V^T operand (A of O^T) through ds_read_b64_tr_b16: a 16-lane group reads a 4-key x
+    // 16-column block and each lane receives its column's 4 keys
     const int q4 = (lane & 15) >> 2;
     int voff[2][ND];
 #pragma unroll
     for (int part = 0; part < 2; ++part)
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
-            const int r = 4 * hh + q4 + 8 * part;
-            const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            if constexpr (MR == 32) {
+                const int r = 4 * hh + q4 + 8 * part;
+                const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+                voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            } else {
+                const int r = 4 * hh + q4 + 16 * part;  // keys 4g.. and 16+4g.. of the tile
+                const int col = 16 * dt + 4 * (lane & 3);
+                voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            }
         }
 
-    f32x16 acc_o[ND];
+    accv acc_o[ND];
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt) acc_o[dt] = f32x16{};
+    for (int dt = 0; dt < ND; ++dt) acc_o[dt] = accv{};
     float m_run = -INFINITY, l_run = 0.f;
 
     // prologue: RING tiles in flight, pages of the next one fetched
     if (t_lo < t_hi) {
 #pragma unroll
         for (int r = 0; r < RING; ++r) {
-            int pg[2];
+            int pg[3] = {0, 0, 0};
             fetch_pages(min(t_lo + r, t_hi - 1), pg);
             issue(min(t_lo + r, t_hi - 1), pg, kraw[r], vraw[r]);
             __builtin_amdgcn_sched_barrier(0);    // slot order = issue order (waitcnt merge)
@@ -203,7 +262,7 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NLD * RING));
 
     // one tile; `slot` is compile-time (the ring is unrolled)
-    auto tile = [&](auto SLOT, const int t) {
+    auto tile = [&](auto SLOT, const int t) __attribute__((always_inline)) {
         constexpr int slot = decltype(SLOT)::value;
         // raw chunks -> T -> LDS images (fp8: 16 values = two 8-element chunks)
 #pragma unroll
@@ -232,30 +291,42 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
         // compiler's loop-header waitcnt merge drain the whole ring every tile)
         issue(min(t + RING, t_hi - 1), pg_next, kraw[slot], vraw[slot]);
         fetch_pages(min(t + RING + 1, t_hi - 1), pg_next);
-        V8 kf[NS];
+        // S^T = K Q^T: MR = 32 one 32x32 block of 32 keys; MR = 16 two 16x16 blocks
+        constexpr int NKB = MR == 32 ? 1 : 2;
+        accv st[NKB];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) kf[s] = *reinterpret_cast<const V8*>(ksl + koff[s]);
-        // S^T = K Q^T
-        f32x16 st{};
+        for (int kb = 0; kb < NKB; ++kb) {
+            V8 kf[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) st = DT<T>::mfma32(kf[s], qf[s], st);
-        // scale / transforms / mask
-        const int keyb = t * kDecKeys + 4 * hh;
-        const bool edge = (t + 1) * kDecKeys > min(sk, my_lr) || t * kDecKeys < my_ll;
+            for (int s = 0; s < NS; ++s) kf[s] = *reinterpret_cast<const V8*>(ksl + koff[s] + kb * 16 * HD * 2);
+            st[kb] = accv{};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float x = st[r];
-            if (KV8) x *= p.k_scale;
-            if (p.softcap_pre > 0.f) x = fast_tanh(x * p.softcap_pre);
-            const int key = keyb + (r & 3) + 8 * (r >> 2);
-            if (p.alibi) x -= alibi_w * (float)abs(pos + diag - key);
-            if (edge && (key >= my_lr || key < my_ll)) x = -INFINITY;
-            st[r] = x;
+            for (int s = 0; s < NS; ++s) {
+                if constexpr (MR == 32) st[kb] = DT<T>::mfma32(kf[s], qf[s], st[kb]);
+                else st[kb] = dec_mfma16<T>(kf[s], qf[s], st[kb]);
+            }
         }
-        float mx = st[0];
+        // scale / transforms / mask; element (kb, r) is key t*32 + keyof(kb, r)
+        auto keyof = [&](const int kb, const int r) {
+            return MR == 32 ? 4 * hh + (r & 3) + 8 * (r >> 2) : 16 * kb + 4 * hh + r;
+        };
+        const int keyb = t * kDecKeys;
+        const bool edge = (t + 1) * kDecKeys > min(sk, my_lr) || t * kDecKeys < my_ll;
+        float mx = -INFINITY;
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[r]);
-        mx = wave_max_halves(mx);
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int r = 0; r < NA; ++r) {
+                float x = st[kb][r];
+                if (KV8) x *= p.k_scale;
+                if (p.softcap_pre > 0.f) x = fast_tanh(x * p.softcap_pre);
+                const int key = keyb + keyof(kb, r);
+                if (p.alibi) x -= alibi_w * (float)abs(pos + diag - key);
+                if (edge && (key >= my_lr || key < my_ll)) x = -INFINITY;
+                st[kb][r] = x;
+                mx = fmaxf(mx, x);
+            }
+        mx = MR == 32 ? wave_max_halves(mx) : quad_max16(mx);
         const float m_new = fmaxf(m_run, mx);
         const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
         if (__any(m_new > m_run)) {
@@ -264,46 +335,48 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
 #pragma unroll
             for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+                for (int r = 0; r < NA; ++r) acc_o[dt][r] *= alpha;
             m_run = m_new;
         }
-        V8 pb[2];
+        // P -> T: the B operand of the PV product (keys permuted as in the header comment)
+        constexpr int NPB = MR == 32 ? 2 : 1;
+        V8 pb[NPB];
         float rs = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float e = fast_exp2(fmaf(st[r], c, -mref));
-            rs += e;
-            pb[r >> 3][r & 7] = (T)e;
-        }
-        l_run += rs;
-        // O^T += V^T P^T (keys permuted as in fmha_fwd_kernel.h)
+        for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-        for (int sp = 0; sp < 2; ++sp)
+            for (int r = 0; r < NA; ++r) {
+                const float e = fast_exp2(fmaf(st[kb][r], c, -mref));
+                rs += e;
+                const int i = kb * NA + r;
+                pb[i >> 3][i & 7] = (T)e;
+            }
+        l_run += rs;
+        // O^T += V^T P^T
+#pragma unroll
+        for (int sp = 0; sp < NPB; ++sp)
 #pragma unroll
             for (int dt = 0; dt < ND; ++dt) {
                 const char* b = vsl + 16 * sp * HD * 2;
                 const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[0][dt]));
                 const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[1][dt]));
                 const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-                acc_o[dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb[sp], acc_o[dt]);
+                if constexpr (MR == 32) acc_o[dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb[sp], acc_o[dt]);
+                else acc_o[dt] = dec_mfma16<T>(__builtin_bit_cast(V8, av), pb[sp], acc_o[dt]);
             }
     };
 
+    // whole groups of RING tiles in a loop without a mid-body exit (keeps the waitcnt merge
+    // exact), then the remainder, which starts again at slot 0
     int t = t_lo;
-    if constexpr (RING == 2) {
-        // whole pairs in a loop without a mid-body exit (keeps the waitcnt merge exact), then
-        // the odd last tile
-        for (; t + 1 < t_hi; t += 2) {
-            tile(std::integral_constant<int, 0>{}, t);
-            tile(std::integral_constant<int, 1>{}, t + 1);
-        }
-        if (t < t_hi) tile(std::integral_constant<int, 0>{}, t);
-    } else {
-        for (; t < t_hi; ++t) tile(std::integral_constant<int, 0>{}, t);
-    }
+    for (; t + RING - 1 < t_hi; t += RING)
+        static_for<RING>([&](auto S) { tile(S, t + decltype(S)::value); });
+    static_for<RING - 1>([&](auto S) {
+        if (t + decltype(S)::value < t_hi) tile(S, t + decltype(S)::value);
+    });
 
     // ---- split partial: O (fp32, normalised, v_scale applied) + LSE; empty -> O = 0, -inf
-    const float l_full = wave_sum_halves(l_run);
+    const float l_full = MR == 32 ? wave_sum_halves(l_run) : quad_sum16(l_run);
     const bool empty = (l_full == 0.f) || (l_full != l_full);
     const float inv = empty ? 0.f : (KV8 ? p.v_scale : 1.f) / l_full;
     if (!row_ok) return;
@@ -312,8 +385,9 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int d = 32 * dt + 8 * g + 4 * hh;
+        for (int g = 0; g < NA / 4; ++g) {
+            // O^T element (dt, 4g + v): d = 32 dt + 8 g + 4 hh + v (MR 32), 16 dt + 4 hh + v (MR 16)
+            const int d = MR == 32 ? 32 * dt + 8 * g + 4 * hh : 16 * dt + 4 * hh;
             *reinterpret_cast<f32x4*>(oa + d) = f32x4{acc_o[dt][4 * g] * inv, acc_o[dt][4 * g + 1] * inv,
                                                       acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv};
         }

@@ -43,8 +43,15 @@ template <int HD, typename T>
 static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
     dim3 grid(p.b * p.hk, p.num_splits / kDecWaves);
-    if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true>), grid, dim3(kDecWaves * 64), smem, st, p);
-    else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false>), grid, dim3(kDecWaves * 64), smem, st, p);
+    // GQA groups of <= 16 query rows run the 16x16x32 tile (fmha_decode_kernel.h, MR = 16)
+    const bool r16 = p.seqlen_q * p.group <= 16 && options().fwd_decode16;
+    if (p.kv_fp8) {
+        if (r16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
+        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+    } else {
+        if (r16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
+        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);

@@ -33,14 +33,6 @@ namespace xfa {
 #endif
 constexpr bool SCHED_FENCE = XFA_SCHED_FENCE;
 
-// Compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>).
-template <int N, int I = 0, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<N, I + 1>(f);
-    }
-}
 
 // One work item = (batch x kv-head, query row block, split).
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
@@ -634,31 +626,51 @@ __global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p)
 // One wave per (b, h, pos) row.
 template <int HD, typename T>
 __global__ void __launch_bounds__(256) fmha_combine_kernel(const CombineParams cp) {
+    // The split partials are independent loads: the LSE reduction runs with the splits across
+    // the lanes, and the O sum keeps CU = 8 splits' rows in flight per wave (a serial loop over
+    // splits exposes one load latency per split, which at 32 splits cost more than the bytes).
     const int lane = threadIdx.x & 63;
-    const int64_t rid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t rid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t rows = (int64_t)cp.b * cp.h * cp.seqlen_q;
     if (rid >= rows) return;
     const int pos = (int)(rid % cp.seqlen_q);
     const int head = (int)((rid / cp.seqlen_q) % cp.h);
     const int bidx = (int)(rid / ((int64_t)cp.seqlen_q * cp.h));
+    const int ns = cp.num_splits;
     float mx = -INFINITY;
-    for (int s = 0; s < cp.num_splits; ++s) mx = fmaxf(mx, cp.lseaccum[s * rows + rid]);
+    for (int s = lane; s < ns; s += 64) mx = fmaxf(mx, cp.lseaccum[s * rows + rid]);
+    mx = wave_max_halves(mx);
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
     float sum = 0.f;
     if (mx != -INFINITY)
-        for (int s = 0; s < cp.num_splits; ++s) sum += __expf(cp.lseaccum[s * rows + rid] - mx);
+        for (int s = lane; s < ns; s += 64) sum += __expf(cp.lseaccum[s * rows + rid] - mx);
+    sum = wave_sum_halves(sum);
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
     const bool empty = (mx == -INFINITY) || sum == 0.f;
     const float lse = empty ? INFINITY : __logf(sum) + mx;
     constexpr int PER = HD / 64;
-    float acc[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) acc[i] = 0.f;
+    constexpr int CU = 8;
+    typedef float __attribute__((ext_vector_type(PER))) fv;
+    fv acc = {};
     if (!empty) {
-        for (int s = 0; s < cp.num_splits; ++s) {
-            const float w = __expf(cp.lseaccum[s * rows + rid] - lse);
-            const float* oa = cp.oaccum + (s * rows + rid) * HD + lane * PER;
+        const float* oa = cp.oaccum + rid * HD + lane * PER;
+        const int64_t sstride = rows * HD;
+        int s = 0;
+        for (; s + CU <= ns; s += CU) {
+            fv x[CU];
+            float w[CU];
 #pragma unroll
-            for (int i = 0; i < PER; ++i) acc[i] = fmaf(w, oa[i], acc[i]);
+            for (int u = 0; u < CU; ++u) {
+                x[u] = *reinterpret_cast<const fv*>(oa + (s + u) * sstride);
+                w[u] = __expf(cp.lseaccum[(s + u) * rows + rid] - lse);
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) acc += w[u] * x[u];
         }
+        for (; s < ns; ++s)
+            acc += __expf(cp.lseaccum[s * rows + rid] - lse) * *reinterpret_cast<const fv*>(oa + s * sstride);
     }
     T* orow = reinterpret_cast<T*>(cp.o) + (int64_t)bidx * cp.o_batch + (int64_t)pos * cp.o_row +
               (int64_t)head * cp.o_head;
