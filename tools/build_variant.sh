@@ -1,17 +1,12 @@
 #!/bin/bash
-# Build the library with a replacement kernel header and park it as a named variant for
-# tools/lib_ab.py:  bash tools/build_variant.sh <name> <header-file> [target-header-name]
-# (the tree is restored and rebuilt afterwards).
+# Build the library with extra compile flags and park it as a named variant for
+# tools/lib_ab.py:  bash tools/build_variant.sh <name> "<flags>"   e.g. "-DXFA_EXP_SCALAR=2"
+# (objects are rebuilt with the flags, then the default build is restored).
 set -e
 cd "$(dirname "$0")/.."
-name=$1; hdr=$2; tgt=${3:-fmha_fwd_kernel.h}
-C=xf_flash_attention_cutlass_amd/csrc
+name=$1; flags=$2
 mkdir -p variants
-cp $C/$tgt /tmp/_variant_keep.h
-cp "$hdr" $C/$tgt
-python -c "from xf_flash_attention_cutlass_amd import build; build.build_lib()" 
+XFA_EXTRA_FLAGS="$flags" python -c "from xf_flash_attention_cutlass_amd import build; build.build_lib(force=True)"
 cp xf_flash_attention_cutlass_amd/lib/libpaged-attention.so variants/lib_$name.so
-cp /tmp/_variant_keep.h $C/$tgt
-touch $C/$tgt
-python -c "from xf_flash_attention_cutlass_amd import build; build.build_lib()"
+python -c "from xf_flash_attention_cutlass_amd import build; build.build_lib(force=True)"
 echo "variants/lib_$name.so"

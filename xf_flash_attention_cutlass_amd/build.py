@@ -31,6 +31,8 @@ LIBNAME = "libpaged-attention.so"
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-I", CSRC, "-I", INCLUDE]
+# extra -D/-f flags for A/B variants of the library (tools/build_variant.sh); not for releases
+HIP_FLAGS += os.environ.get("XFA_EXTRA_FLAGS", "").split()
 
 VARIANTS = [(hd, dt) for hd in (64, 128) for dt in ("bf16", "f16")]
 
