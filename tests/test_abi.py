@@ -70,7 +70,7 @@ def _fwd(**over):
     (dict(b=0), "batch size"),
     (dict(h=3, hk=2), "must divide"),
     (dict(d=60), "multiple of 8"),
-    (dict(d=512), "not supported"),
+    (dict(d=512), "at most 256"),
     (dict(p=0.1), "dropout"),
     (dict(sk=0), "positive"),
 ])

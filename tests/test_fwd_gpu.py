@@ -535,3 +535,105 @@ def test_fwd_persistent_order_bitexact(xfa, cfg):
                                   upcast=False, reorder_ops=True)
         _assert_parity(outs[-1][0][:1, :, :4].float().cpu(), r.cpu(), pt.float().cpu(),
                        what=str(cfg))
+
+
+# ------------------------------------------------------------------- head dims 129..256 ---
+# The reference dispatches head-dim buckets up to 256 (static_switch.h:90-117); D in
+# (128, 256] runs the 4-wave, 512-register build of the forward kernel.
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [136, 160, 192, 256])
+@pytest.mark.parametrize("sq,sk,h,hk", [(1, 147, 4, 4), (113, 203, 4, 2), (300, 300, 6, 3),
+                                        (1023, 1024, 2, 2)])
+def test_fwd_large_head_dims(xfa, dtype, causal, d, sq, sk, h, hk):
+    q, k, v, out_ref, out_pt = _rand_case(1, h, hk, sq, sk, d, dtype, causal, seed=d)
+    out, lse, _ = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal,
+                                      return_attn_probs=True)
+    assert out.shape == (1, sq, h, d)
+    _assert_parity(out, out_ref, out_pt, what=f"{sq}x{sk} h{h}/{hk} d{d} c{causal}")
+    lse_ref = orc.attention_lse_ref(q, k, causal=causal)
+    fin = torch.isfinite(lse_ref)
+    assert torch.equal(torch.isinf(lse.cpu()), ~fin)
+    assert (lse.cpu()[fin] - lse_ref[fin]).abs().max().item() < LSE_ATOL
+
+
+@pytest.mark.parametrize("window", [(17, 3), (-1, 40)])
+def test_fwd_d256_windows_alibi_softcap(xfa, window):
+    torch.manual_seed(3)
+    b, h, hk, sq, sk, d = 2, 4, 2, 211, 333, 256
+    q = torch.randn(b, sq, h, d).bfloat16()
+    k = torch.randn(b, sk, hk, d).bfloat16()
+    v = torch.randn(b, sk, hk, d).bfloat16()
+    slopes = torch.rand(b, h) * 0.3
+    w = oracle_window(window, sk)
+    bias = orc.alibi_bias(slopes, sq, sk, causal=False)
+    r, _ = orc.attention_ref(q, k, v, attn_bias=bias, window_size=w, softcap=30.0)
+    pt, _ = orc.attention_ref(q, k, v, attn_bias=bias, window_size=w, softcap=30.0,
+                              upcast=False, reorder_ops=True)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), window_size=window,
+                              softcap=30.0, alibi_slopes=slopes.to(DEV))
+    _assert_parity(out, r, pt, what=f"d256 window {window} alibi softcap")
+
+
+@pytest.mark.parametrize("splits", [2, 5])
+def test_fwd_d256_split_kv(xfa, splits):
+    torch.manual_seed(1)
+    q = torch.randn(2, 64, 4, 256, dtype=torch.bfloat16, device=DEV)
+    k = torch.randn(2, 1500, 2, 256, dtype=torch.bfloat16, device=DEV)
+    v = torch.randn(2, 1500, 2, 256, dtype=torch.bfloat16, device=DEV)
+    one = xfa.flash_attn_with_kvcache(q, k, v, causal=True, num_splits=1)
+    many = xfa.flash_attn_with_kvcache(q, k, v, causal=True, num_splits=splits)
+    assert (one.float() - many.float()).abs().max().item() < 2e-2
+    r, _ = orc.attention_ref(q.cpu(), k.cpu(), v.cpu(), causal=True)
+    pt, _ = orc.attention_ref(q.cpu(), k.cpu(), v.cpu(), causal=True, upcast=False, reorder_ops=True)
+    _assert_parity(many, r, pt, mult=3.0, atol=1e-5, what=f"d256 splits {splits}")
+
+
+def test_varlen_d192(xfa):
+    torch.manual_seed(2)
+    h, hk, d = 4, 1, 192
+    lq, lk = [1, 257, 64, 700], [90, 257, 1, 700]
+    cu_q = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(sum(lq), h, d).half()
+    k = torch.randn(sum(lk), hk, d).half()
+    v = torch.randn(sum(lk), hk, d).half()
+    for causal in (False, True):
+        out = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu_q.to(DEV),
+                                         cu_k.to(DEV), max(lq), max(lk), causal=causal).cpu()
+        for i in range(len(lq)):
+            qs = q[cu_q[i]:cu_q[i + 1]][None]
+            ks, vs = k[cu_k[i]:cu_k[i + 1]][None], v[cu_k[i]:cu_k[i + 1]][None]
+            r, _ = orc.attention_ref(qs, ks, vs, causal=causal)
+            pt, _ = orc.attention_ref(qs, ks, vs, causal=causal, upcast=False, reorder_ops=True)
+            _assert_parity(out[cu_q[i]:cu_q[i + 1]][None], r, pt, what=f"d192 seq {i} c{causal}")
+
+
+@pytest.mark.parametrize("sq", [1, 5])
+def test_paged_d256_bitexact(xfa, sq):
+    """Paged decode at D = 256 (general kernel, split-KV) == dense gather, bit for bit."""
+    torch.manual_seed(4)
+    b, h, hk, d, page, sk = 3, 8, 2, 256, 16, 700
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    q = torch.randn(b, sq, h, d).bfloat16().to(DEV)
+    seqlens = torch.tensor([700, 301, 17], dtype=torch.int32).to(DEV)
+    paged = xfa.flash_attn_with_kvcache(q, kp.to(DEV), vp.to(DEV), cache_seqlens=seqlens,
+                                        block_table=table.to(DEV))
+    nblk = table.shape[1]
+    kfull = kp[table.long().flatten()].reshape(b, nblk * page, hk, d).to(DEV)
+    vfull = vp[table.long().flatten()].reshape(b, nblk * page, hk, d).to(DEV)
+    dense = xfa.flash_attn_with_kvcache(q, kfull, vfull, cache_seqlens=seqlens)
+    assert torch.equal(paged, dense)
+    kpm = torch.arange(sk).view(1, -1) < seqlens.cpu().view(-1, 1)
+    r, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm)
+    pt, _ = orc.attention_ref(q.cpu(), kc, vc, None, kpm, upcast=False, reorder_ops=True)
+    _assert_parity(paged, r, pt, mult=3.0, atol=1e-5, what="paged d256")
+
+
+def test_d256_backward_rejected(xfa):
+    q = torch.randn(1, 64, 2, 256, dtype=torch.bfloat16, device=DEV, requires_grad=True)
+    k = torch.randn(1, 64, 2, 256, dtype=torch.bfloat16, device=DEV, requires_grad=True)
+    v = torch.randn(1, 64, 2, 256, dtype=torch.bfloat16, device=DEV, requires_grad=True)
+    out = xfa.flash_attn_func(q, k, v, causal=True)
+    with pytest.raises(RuntimeError, match="at most 128"):
+        out.sum().backward()

@@ -34,7 +34,8 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-f
 # extra -D/-f flags for A/B variants of the library (tools/build_variant.sh); not for releases
 HIP_FLAGS += os.environ.get("XFA_EXTRA_FLAGS", "").split()
 
-VARIANTS = [(hd, dt) for hd in (64, 128) for dt in ("bf16", "f16")]
+VARIANTS = [(hd, dt) for hd in (64, 128, 256) for dt in ("bf16", "f16")]
+BWD_HDS = (64, 128)          # the backward covers head dims <= 128
 
 
 def _newer(out: str, deps) -> bool:
@@ -65,7 +66,7 @@ def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     todo = []
     for hd, dt in VARIANTS:
         defs = [f"-DXFA_HD={hd}", f"-DXFA_DTN={dt}", f"-DXFA_DT_BF16={1 if dt == 'bf16' else 0}"]
-        for kind in ("fwd", "bwd"):
+        for kind in (("fwd", "bwd") if hd in BWD_HDS else ("fwd",)):
             src = os.path.join(CSRC, f"fmha_{kind}.hip")
             todo.append((src, os.path.join(OBJ, f"fmha_{kind}_hd{hd}_{dt}.o"), defs))
     todo.append((os.path.join(CSRC, "fmha_append.hip"), os.path.join(OBJ, "fmha_append.o"), []))

@@ -116,6 +116,7 @@ hipError_t dispatch_fwd(const FwdParams& p, bool bf16, hipStream_t st) {
     const int hd = hd_bucket(p.d);
     if (hd == 64) return bf16 ? launch_fwd_hd64_bf16(p, st) : launch_fwd_hd64_f16(p, st);
     if (hd == 128) return bf16 ? launch_fwd_hd128_bf16(p, st) : launch_fwd_hd128_f16(p, st);
+    if (hd == 256) return bf16 ? launch_fwd_hd256_bf16(p, st) : launch_fwd_hd256_f16(p, st);
     return hipErrorInvalidValue;
 }
 
@@ -149,7 +150,7 @@ bool check_common(const void* q, const void* k, const void* v, const void* o, in
     if (h <= 0 || hk <= 0 || h % hk != 0)
         return fail(1, "Number of heads in key/value must divide number of heads in query (h=%d, hk=%d)", h, hk);
     if (d <= 0 || d % 8 != 0) return fail(1, "head_size must be a positive multiple of 8 (got %d)", d);
-    if (d > 128) return fail(1, "head_size %d not supported by this build (max 128)", d);
+    if (d > 256) return fail(1, "FlashAttention forward only supports head dimension at most 256 (got %d)", d);
     return true;
 }
 
@@ -168,7 +169,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     // Decode: the whole GQA group of query rows fits one 32-row MFMA tile -> the split-KV
     // decode kernel (every wave a split, fmha_decode_kernel.h); splits a multiple of 4.
     p.decode = options().fwd_decode && !p.cu_seqlens_q && !p.cu_seqlens_k &&
-               p.seqlen_q * p.group <= 32 && hd_bucket(p.d) == p.d &&
+               p.seqlen_q * p.group <= 32 && hd_bucket(p.d) == p.d && p.d <= 128 &&
                (!p.block_table || p.page_size % 16 == 0);
     if (p.decode) {
         const int tiles = (p.seqlen_k + 31) / 32;
@@ -181,7 +182,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     } else if (p.cu_seqlens_q) {
         splits = 1;  // varlen: single pass (the reference forces it too)
     } else if (splits <= 0) {
-        const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group);
+        const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group, p.d);
         splits = num_splits_heuristic(work, num_cus() * 2, n_blocks, 128);
     }
     if (!p.decode) splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
@@ -481,6 +482,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(head_size <= 128, "this build's backward supports head dimension at most 128 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
         REQUIRE(p_dropout == 0.f, "dropout is not supported by the backward (p_dropout=%g)", p_dropout);
@@ -529,6 +531,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(head_size <= 128, "this build's backward supports head dimension at most 128 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
         REQUIRE(cu_seqlens_q && cu_seqlens_k, "cu_seqlens_q/cu_seqlens_k must be non-null");
         REQUIRE(total_q > 0 && total_k > 0 && max_seqlen_q > 0 && max_seqlen_k > 0,

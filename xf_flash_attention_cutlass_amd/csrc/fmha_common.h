@@ -48,6 +48,9 @@ __device__ __forceinline__ u32x2 buf_load8(__amdgpu_buffer_rsrc_t r, int voff) {
 }
 
 constexpr int kBlockN = 64;   // keys per K/V tile (one LDS stage)
+// forward LDS buffers per K/V tile pair and waves per SIMD, by head-dim bucket
+constexpr int fwd_nbuf(int hd) { return hd > 128 ? 2 : 4; }
+constexpr int fwd_waves_per_simd(int hd) { return hd > 128 ? 1 : 2; }
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -175,6 +178,11 @@ template <> __device__ __forceinline__ int swz<128>(int row) {
 }
 template <> __device__ __forceinline__ int swz<64>(int row) {
     return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+// D = 256 rows are 512 B (also a whole number of bank rows): the D = 128 pattern on the low
+// four chunk bits keeps the 32-row ds_read_b128 and the transposing reads conflict-free
+template <> __device__ __forceinline__ int swz<256>(int row) {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
 }
 template <int HD> __device__ __forceinline__ int lds_off(int row, int chunk) {
     return row * (HD * 2) + ((chunk ^ swz<HD>(row)) << 4);

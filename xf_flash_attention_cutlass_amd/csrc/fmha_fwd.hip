@@ -76,7 +76,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
             grid = dim3(slots, 1, grid.z);
         }
     }
-    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(4 * 2 * kBlockN * HD * 2);
+    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(fwd_nbuf(HD) * 2 * kBlockN * HD * 2);
     void (*kern)(const FwdParams);
     if constexpr (PP) {
         const int sm = options().fwd_sched;
@@ -112,10 +112,15 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 }
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
+#if XFA_HD > 128
+    // D = 256: 4-wave register-staged kernel only (no decode / ping-pong / DMA pipeline)
+    return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
+#else
     if (p.decode) return launch_decode<XFA_HD, elem_t>(p, st);
     if (options().fwd_pp && !p.kv_fp8) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
     if (options().fwd_waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8, false>(p, st);
     return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
+#endif
 }
 
 }  // namespace xfa

@@ -44,7 +44,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     constexpr int CPR = HD / 8;                 // 16-byte chunks per K/V row
     constexpr int NLD = kBlockN * CPR / NT;     // chunks per thread per tile
     constexpr int TILE = kBlockN * HD * 2;      // bytes of one K (or V) tile
-    constexpr int NBUF = 4;                     // LDS buffers (K and V tile each)
+    // LDS buffers (K and V tile each): D <= 128 runs the 4-buffer LDS-DMA pipeline; D = 256
+    // (32 KiB tiles) only the double-buffered register-staged loop, 128 KiB of LDS
+    constexpr int NBUF = fwd_nbuf(HD);
+    constexpr bool PIPE = HD <= 128;
     constexpr int VREG = NBUF * TILE;           // LDS: K tiles of buffers 0..3, then V tiles
     constexpr int NS = HD / 16;                 // k-steps of the QK^T product
     constexpr int ND = HD / 32;                 // 32-wide d tiles of O^T
@@ -538,7 +541,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // [f_lo, f_hi) every row of the workgroup sees in full; [f_hi, nb_hi) cross the right
     // window edge / the end of the keys.  The last two ranges run through the pipeline.
     int f_lo = nb_hi, f_hi = nb_hi;
-    if (p.pipe && !paged && !kv8) {
+    if (PIPE && p.pipe && !paged && !kv8) {
         const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
         f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
         f_hi = max(f_lo, min(nb_hi, lr_min / kBlockN));
@@ -548,7 +551,9 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // (fwd_pipe=2: edge tiles through the per-wave masked loop instead - A/B knob)
     const int p_hi = (p.pipe == 2 && f_hi - f_lo >= 2) ? f_hi : nb_hi;
     masked_range(nb_lo, f_lo);
-    if (f_lo < p_hi) pipe_range(f_lo, f_hi, p_hi);
+    if constexpr (PIPE) {
+        if (f_lo < p_hi) pipe_range(f_lo, f_hi, p_hi);
+    }
     masked_range(p_hi, nb_hi);
 
     // ---- epilogue: normalise, write O (or the split partial) and LSE
@@ -588,7 +593,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
 // causal work per workgroup balances, and one item's O-store tail overlaps the next item's
 // prologue loads instead of a workgroup boundary.
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
-__global__ void __launch_bounds__(NW * 64, 2) fmha_fwd_kernel(const FwdParams p) {
+__global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;

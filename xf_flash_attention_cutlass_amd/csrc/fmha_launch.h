@@ -32,6 +32,8 @@ hipError_t launch_fwd_hd64_bf16(const FwdParams& p, hipStream_t st);
 hipError_t launch_fwd_hd64_f16(const FwdParams& p, hipStream_t st);
 hipError_t launch_fwd_hd128_bf16(const FwdParams& p, hipStream_t st);
 hipError_t launch_fwd_hd128_f16(const FwdParams& p, hipStream_t st);
+hipError_t launch_fwd_hd256_bf16(const FwdParams& p, hipStream_t st);
+hipError_t launch_fwd_hd256_f16(const FwdParams& p, hipStream_t st);
 
 // Backward (preprocess + main + convert) for head dim bucket HD.
 hipError_t launch_bwd_hd64_bf16(const BwdParams& p, hipStream_t st);
@@ -54,9 +56,14 @@ struct AppendParams {
 };
 hipError_t launch_append(const AppendParams& p, bool fp16, hipStream_t st);
 
-inline int fwd_block_m() { return options().fwd_pp ? 256 : options().fwd_waves * 32; }
-inline int fwd_num_m_blocks(int seqlen_q, int group) {
-    return (seqlen_q * group + fwd_block_m() - 1) / fwd_block_m();
+// D = 256 (bucket of 129..256): 4 waves x 32 rows, one wave per SIMD (512 registers:
+// Q fragments and the O accumulator alone are 192), no LDS-DMA pipeline
+inline int fwd_block_m(int d) {
+    if (d > 128) return 128;
+    return options().fwd_pp ? 256 : options().fwd_waves * 32;
+}
+inline int fwd_num_m_blocks(int seqlen_q, int group, int d) {
+    return (seqlen_q * group + fwd_block_m(d) - 1) / fwd_block_m(d);
 }
 
 }  // namespace xfa

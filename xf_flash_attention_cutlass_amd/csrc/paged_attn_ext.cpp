@@ -84,7 +84,7 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     const int seqlen_k = k.size(1);
     const int num_heads_k = k.size(2);
     TORCH_CHECK(batch_size > 0, "batch size must be postive");
-    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
     TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
@@ -165,7 +165,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     const int num_heads_k = paged_KV ? k.size(2) : k.size(1);
     const int total_q = sizes[0];
     TORCH_CHECK(batch_size > 0, "batch size must be positive");
-    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
     TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
@@ -276,7 +276,7 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
     const int seqlen_k = max_num_blocks_per_seq * page_block_size;
     const int num_heads_k = kcache.size(2);
     TORCH_CHECK(batch_size > 0, "batch size must be positive");
-    TORCH_CHECK(head_size_og <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     if (seqlen_q == 1 && !alibi_slopes_.has_value()) is_causal = false;
     if (is_causal) window_size_right = 0;
@@ -423,7 +423,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     const int num_heads_k = k.size(2);
     TORCH_CHECK(batch_size > 0, "batch size must be positive");
     TORCH_CHECK(head_size % 8 == 0, "head_size should be a multiple of 8");
-    TORCH_CHECK(head_size <= 128, "this build supports head dimension at most 128");
+    TORCH_CHECK(head_size <= 128, "this build's backward supports head dimension at most 128");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(head_size == round8(head_size_og), "head_size must be head_size_og rounded to a multiple of 8");
     if (window_size_left >= seqlen_k) window_size_left = -1;
@@ -554,7 +554,7 @@ mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& v
                 "block_table / seqlens_k must be int32");
     const int batch_size = q.size(0), seqlen_q = q.size(1), num_heads = q.size(2), d = q.size(3);
     const int page = kcache.size(1), num_heads_k = kcache.size(2);
-    TORCH_CHECK(kcache.size(3) == d && d % 8 == 0 && d <= 128, "head_size must be a multiple of 8 and <= 128");
+    TORCH_CHECK(kcache.size(3) == d && d % 8 == 0 && d <= 256, "head_size must be a multiple of 8 and <= 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     CHECK_SHAPE(block_table, batch_size, block_table.size(1));
     CHECK_SHAPE(seqlens_k, batch_size);
