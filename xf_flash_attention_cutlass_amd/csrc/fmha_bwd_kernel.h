@@ -201,7 +201,12 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     uint4 qreg[QLD], doreg[QLD];
     // LSE (lanes 0-31, pre-multiplied by log2e) and D = rowsum(dO*O) (lanes 32-63) of the
     // tile's 32 rows: one load per lane, prefetched with Q/dO, fetched by ds_bpermute
-    float lsd_next = 0.f;
+    // The raw value is kept until the end of the iteration: converting it right after the
+    // load makes the wave wait vmcnt on it, and vmcnt is in order, so that wait would also
+    // retire the previous tile's dQ atomics (thousands of cycles with every CU issuing).
+    float lsd_raw = 0.f;
+    bool lsd_ok = false;
+    auto lsd_value = [&]() { return hh ? (lsd_ok ? lsd_raw : 0.f) : (lsd_ok ? lsd_raw * kLog2e : INFINITY); };
     auto load_q = [&](int it) {
         const int g = it / ntiles;
         const int tt = it - g * ntiles;
@@ -211,8 +216,8 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             const bool ok = pos < sq;
             const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off +
                                (ok ? pos : 0);
-            const float x = (hh ? p.dsum : p.lse)[li];
-            lsd_next = hh ? (ok ? x : 0.f) : (ok ? x * kLog2e : INFINITY);
+            lsd_raw = (hh ? p.dsum : p.lse)[li];
+            lsd_ok = ok;
         }
         // buffer loads over this head's rows [q0, sq): rows past the end and padded head-dim
         // chunks read as zeros (no branches)
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     float lsd_cur = 0.f;
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible
-    if (n_iter > 0) { store_q(); lsd_cur = lsd_next; }
+    if (n_iter > 0) { store_q(); lsd_cur = lsd_value(); }
     __syncthreads();
 
     for (int it = 0; it < n_iter; ++it) {
@@ -433,7 +438,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             }
         }
         if (it + 1 < n_iter) store_q();
-        lsd_cur = lsd_next;
+        lsd_cur = lsd_value();
         __syncthreads();
     }
 
