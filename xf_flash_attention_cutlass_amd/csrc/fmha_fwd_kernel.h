@@ -429,6 +429,31 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
+    // D = 256 (no pipeline, NBUF = 2): the per-wave masked loop with K/V by LDS-DMA, tile
+    // j+1 in flight while tile j computes (no staging registers: the 512-register budget is
+    // taken by the Q fragments and the O accumulator)
+    auto dma_range = [&](const int lo, const int hi) {
+        if (lo >= hi) return;
+        dma_tile(lo, 0);
+        publish(false);
+        int buf = 0;
+        for (int nb = lo; nb < hi; ++nb) {
+            if (nb + 1 < hi) dma_tile(nb + 1, buf ^ 1);
+            const int n0 = nb * kBlockN;
+            const bool active = wave_ok && n0 < w_lr_max && n0 + kBlockN > w_ll_min;
+            if (active) {
+                f32x16 st[2];
+                qk(buf, st);
+                transform_part(st, n0, (n0 + kBlockN > w_lr_min) || (n0 < w_ll_max), 0, 32);
+                raise_max(row_max(st));
+                V8 pb[4];
+                exp_tile(st, pb);
+                pv(buf, pb);
+            }
+            publish(false);
+            buf ^= 1;
+        }
+    };
     // Tiles [lo, hm) need no mask; tiles [hm, hi) (the causal diagonal / right window edge /
     // ragged end) are masked in registers on the way through the same pipeline (a wave whose
     // rows cannot see such a tile computes zeros for it instead of branching out of the
@@ -550,7 +575,8 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     if (p.prio_hi && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     // (fwd_pipe=2: edge tiles through the per-wave masked loop instead - A/B knob)
     const int p_hi = (p.pipe == 2 && f_hi - f_lo >= 2) ? f_hi : nb_hi;
-    masked_range(nb_lo, f_lo);
+    if (!PIPE && !paged && !kv8) dma_range(nb_lo, f_lo);
+    else masked_range(nb_lo, f_lo);
     if constexpr (PIPE) {
         if (f_lo < p_hi) pipe_range(f_lo, f_hi, p_hi);
     }
