@@ -137,3 +137,58 @@ def test_bwd_capi_workspace_and_errors(xfa):
     capi.check()
     L.fmha_bwd(*args, ws.data_ptr(), 16)
     assert L.fmha_last_status() != 0 and "workspace" in L.fmha_last_error().decode()
+
+
+# Head dims 129..256 (the D = 256 bucket: 4 waves x 32 keys, V rows in registers; the
+# reference's mha_bwd accepts head_size <= 256, flash_api_hip.cpp:883) and padded dims
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [160, 256])
+@pytest.mark.parametrize("sq,sk,h,hk", [(128, 128, 2, 2), (113, 203, 4, 2), (257, 771, 2, 1)])
+def test_bwd_d256_bucket(xfa, dtype, causal, d, sq, sk, h, hk):
+    gen = torch.Generator().manual_seed(3)
+    q = torch.randn(1, sq, h, d, generator=gen).to(dtype)
+    k = torch.randn(1, sk, hk, d, generator=gen).to(dtype)
+    v = torch.randn(1, sk, hk, d, generator=gen).to(dtype)
+    g = torch.randn(1, sq, h, d, generator=gen).to(dtype)
+    got = _run(xfa, q, k, v, g, causal=causal)
+    ref, pt = _oracle_grads(q, k, v, g, causal=causal)
+    for nm, a, r, p in zip(("dq", "dk", "dv"), got, ref, pt):
+        _grad_check(f"{nm} {sq}x{sk} h{h}/{hk} d{d} c{causal}", a, r, p)
+
+
+def test_bwd_d256_local_softcap_alibi(xfa):
+    gen = torch.Generator().manual_seed(4)
+    b, s, h, d = 2, 200, 2, 256
+    q = (torch.randn(b, s, h, d, generator=gen) * 2).bfloat16()
+    k, v, g = (torch.randn(b, s, h, d, generator=gen).bfloat16() for _ in range(3))
+    slopes = torch.rand(b, h, generator=gen) * 0.3
+    bias = orc.alibi_bias(slopes, s, s, causal=False)
+    got = _run(xfa, q, k, v, g, window_size=(48, 16), softcap=30.0, alibi_slopes=slopes.to(DEV))
+    ref, pt = _oracle_grads(q, k, v, g, window_size=(48, 16), softcap=30.0, attn_bias=bias)
+    for nm, a, r, p in zip(("dq", "dk", "dv"), got, ref, pt):
+        _grad_check(f"{nm} d256 local+softcap+alibi", a, r, p, mult=5.0)
+
+
+def test_bwd_d256_varlen(xfa):
+    torch.manual_seed(5)
+    h, hk, d = 4, 2, 192
+    lq, lk = [1, 130, 77, 300], [147, 130, 300, 300]
+    cu_q = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(sum(lq), h, d).bfloat16()
+    k = torch.randn(sum(lk), hk, d).bfloat16()
+    v = torch.randn(sum(lk), hk, d).bfloat16()
+    g = torch.randn(sum(lq), h, d).bfloat16()
+    qd, kd, vd = (x.to(DEV).requires_grad_(True) for x in (q, k, v))
+    out = xfa.flash_attn_varlen_func(qd, kd, vd, cu_q.to(DEV), cu_k.to(DEV), max(lq), max(lk),
+                                     causal=True)
+    dq, dk, dv = (x.cpu() for x in torch.autograd.grad(out, (qd, kd, vd), g.to(DEV)))
+    for i in range(len(lq)):
+        qs, gs = q[cu_q[i]:cu_q[i + 1]][None], g[cu_q[i]:cu_q[i + 1]][None]
+        ks, vs = k[cu_k[i]:cu_k[i + 1]][None], v[cu_k[i]:cu_k[i + 1]][None]
+        ref, pt = _oracle_grads(qs, ks, vs, gs, causal=True)
+        got = (dq[cu_q[i]:cu_q[i + 1]][None], dk[cu_k[i]:cu_k[i + 1]][None],
+               dv[cu_k[i]:cu_k[i + 1]][None])
+        for nm, a, r, p in zip(("dq", "dk", "dv"), got, ref, pt):
+            _grad_check(f"varlen d192 seq{i} {nm}", a, r, p)

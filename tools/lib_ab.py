@@ -63,6 +63,22 @@ def main():
                          a.s, a.s, a.b, a.h, hk, a.d, 0.0, sc, -1, wr, 0.0, False, False, stream,
                          None, 0)
 
+    # outputs of every build against the first one's (atomic dQ sums differ in the last bits
+    # from run to run, so this is a sanity check, not the parity test)
+    ref = None
+    for i, lib in enumerate(libs):
+        for t in (o, dq, dk, dv):
+            t.zero_()
+        run(lib)
+        torch.cuda.synchronize()
+        outs = [t.float().clone() for t in ((o, dq, dk, dv) if a.mode == "bwd" else (o,))]
+        if ref is None:
+            ref = outs
+            continue
+        diffs = " ".join(f"{n}:{(x - r).abs().max().item():.3e}/{r.abs().max().item():.2e}"
+                         for n, x, r in zip(("o", "dq", "dk", "dv"), outs, ref))
+        print(f"check {os.path.basename(a.libs[i])} vs {os.path.basename(a.libs[0])}: {diffs}")
+
     fl = 4.0 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0) * (3.5 if a.mode == "bwd" else 1.0)
     for lib in libs:
         for _ in range(3):

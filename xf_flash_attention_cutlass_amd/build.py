@@ -35,7 +35,7 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-f
 HIP_FLAGS += os.environ.get("XFA_EXTRA_FLAGS", "").split()
 
 VARIANTS = [(hd, dt) for hd in (64, 128, 256) for dt in ("bf16", "f16")]
-BWD_HDS = (64, 128)          # the backward covers head dims <= 128
+BWD_HDS = (64, 128, 256)     # backward head-dim buckets (as the forward)
 
 
 def _newer(out: str, deps) -> bool:

@@ -124,6 +124,7 @@ hipError_t dispatch_bwd(const BwdParams& p, bool bf16, hipStream_t st) {
     const int hd = hd_bucket(p.d);
     if (hd == 64) return bf16 ? launch_bwd_hd64_bf16(p, st) : launch_bwd_hd64_f16(p, st);
     if (hd == 128) return bf16 ? launch_bwd_hd128_bf16(p, st) : launch_bwd_hd128_f16(p, st);
+    if (hd == 256) return bf16 ? launch_bwd_hd256_bf16(p, st) : launch_bwd_hd256_f16(p, st);
     return hipErrorInvalidValue;
 }
 
@@ -482,7 +483,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
-        REQUIRE(head_size <= 128, "this build's backward supports head dimension at most 128 (got %d)", head_size);
+        REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
         REQUIRE(p_dropout == 0.f, "dropout is not supported by the backward (p_dropout=%g)", p_dropout);
@@ -531,7 +532,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
-        REQUIRE(head_size <= 128, "this build's backward supports head dimension at most 128 (got %d)", head_size);
+        REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
         REQUIRE(cu_seqlens_q && cu_seqlens_k, "cu_seqlens_q/cu_seqlens_k must be non-null");
         REQUIRE(total_q > 0 && total_k > 0 && max_seqlen_q > 0 && max_seqlen_k > 0,

@@ -31,7 +31,7 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
     void (*kern)(const BwdParams) =
         mask ? (feat ? fmha_bwd_kernel<HD, T, true, true> : fmha_bwd_kernel<HD, T, true, false>)
              : (feat ? fmha_bwd_kernel<HD, T, false, true> : fmha_bwd_kernel<HD, T, false, false>);
-    const size_t smem = 2 * (size_t)kBwdBlockN * HD * 2 + 2 * (size_t)kBwdBlockM * HD * 2 + kBwdBlockN * 64;
+    const size_t smem = bwd_smem_bytes<HD>();
     static bool attr_done = false;
     if (!attr_done) {
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -40,7 +40,7 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         attr_done = true;
     }
-    const dim3 grid(p.b * p.hk, (p.seqlen_k + kBwdBlockN - 1) / kBwdBlockN);
+    const dim3 grid(p.b * p.hk, (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>());
     hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, p);
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -31,8 +31,36 @@ namespace xfa {
 // so one wave's LDS / global waits hide behind the other's MFMAs.  D = 64 (or
 // XFA_BWD_WAVES=4): 4 waves x 64 keys, one wave per SIMD with 512 registers (a 32-row D=64
 // Q tile has too few 16-byte chunks for 512 threads).
-template <int HD> constexpr int bwd_waves() { return HD >= 128 ? XFA_BWD_WAVES : 4; }
-constexpr int kBwdBlockN = 256;              // keys per workgroup
+template <int HD> constexpr int bwd_waves() { return HD == 128 ? XFA_BWD_WAVES : 4; }
+// Keys per workgroup: 256, or 128 for D = 129..256 (4 waves x 32 keys: the 32 x 256 dK^T and
+// dV^T accumulators take 256 of a wave's 512 registers).
+template <int HD> constexpr int bwd_block_n() { return HD > 128 ? 128 : 256; }
+// D > 128: each wave's V rows (only ever read by that wave, for dP = dO V^T) stay in registers
+// for the whole sweep instead of LDS, so K, Q, dO and dS^T fit the 160 KiB
+template <int HD> constexpr bool bwd_v_in_regs() { return HD > 128; }
+template <int HD> constexpr size_t bwd_smem_bytes() {
+    return (bwd_v_in_regs<HD>() ? 1 : 2) * (size_t)bwd_block_n<HD>() * HD * 2 + 2 * (size_t)32 * HD * 2 +
+           (size_t)bwd_block_n<HD>() * 64;
+}
+#ifndef XFA_BWD_DQ32
+#define XFA_BWD_DQ32 0
+#endif
+#ifndef XFA_BWD_EARLYSTORE
+#define XFA_BWD_EARLYSTORE 1
+#endif
+#ifndef XFA_BWD_NOATOMIC
+#define XFA_BWD_NOATOMIC 0
+#endif
+// dQ partial sums -> the fp32 accumulator (XFA_BWD_NOATOMIC: timing experiment only, the
+// values are consumed but never added)
+__device__ __forceinline__ void dq_atomic_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
+#if XFA_BWD_NOATOMIC
+    asm volatile("" ::"v"(v));
+    (void)r; (void)off;
+#else
+    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
+#endif
+}
 constexpr int kBwdBlockM = 32;               // query rows per tile
 
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
@@ -123,10 +151,11 @@ template <int HD, typename T, bool MASK, bool FEAT>
 __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
     using V8 = typename DT<T>::v8;
     constexpr int NW = bwd_waves<HD>();
-    constexpr int kBwdKeysPerWave = kBwdBlockN / NW;   // keys owned by one wave
+    constexpr int BN = bwd_block_n<HD>();
+    constexpr bool VR = bwd_v_in_regs<HD>();
+    constexpr int kBwdKeysPerWave = BN / NW;   // keys owned by one wave
     constexpr int NT = NW * 64;
     constexpr int KS = kBwdKeysPerWave / 32;     // 32-key subtiles per wave
-    constexpr int BN = kBwdBlockN;
     constexpr int BQ = kBwdBlockM;
     constexpr int CPR = HD / 8;
     constexpr int NS = HD / 16;
@@ -139,8 +168,8 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* k_lds = smem;
-    char* v_lds = smem + KT_BYTES;
-    char* q_lds = v_lds + KT_BYTES;
+    char* v_lds = smem + KT_BYTES;                   // (unused when VR)
+    char* q_lds = smem + (VR ? 1 : 2) * KT_BYTES;
     char* do_lds = q_lds + QT_BYTES;
     char* ds_lds = do_lds + QT_BYTES;
 
@@ -187,12 +216,27 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 y = *reinterpret_cast<const uint4*>(vb + (int64_t)n * p.v_row + c * 8);
             }
             *reinterpret_cast<uint4*>(k_lds + lds_off<HD>(r, c)) = x;
-            *reinterpret_cast<uint4*>(v_lds + lds_off<HD>(r, c)) = y;
+            if (!VR) *reinterpret_cast<uint4*>(v_lds + lds_off<HD>(r, c)) = y;
         }
     }
     int my_key[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) my_key[ks] = n0 + wave * kBwdKeysPerWave + 32 * ks + lr;
+    // VR: this wave's V rows as the B operands of dP = dO V^T (key = lane, d chunk 2s + hh)
+    V8 vfrag[VR ? NS : 1];
+    if constexpr (VR) {
+        static_assert(KS == 1, "V in registers: one 32-key subtile per wave");
+        const T* vb = reinterpret_cast<const T*>(p.v) + (int64_t)bidx * p.v_batch +
+                      (int64_t)k_off * p.v_row + (int64_t)hk_i * p.v_head;
+        const __amdgpu_buffer_rsrc_t vrs = make_rsrc(vb, (uint32_t)(((int64_t)sk * p.v_row) * 2));
+        const int key = my_key[0];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int col = 16 * s + 8 * hh;
+            const int off = (key < sk && col < p.d) ? key * (int)p.v_row * 2 + col * 2 : kOOB;
+            vfrag[s] = __builtin_bit_cast(V8, buf_load16(vrs, off));
+        }
+    }
 
     // ---- Q / dO tile loader (QLD 16-byte chunks of each per thread)
     const int lrow = tid / CPR, lcol = tid % CPR;
@@ -249,23 +293,30 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     };
 
     // per-lane LDS addresses (tile-relative constants fold into the ds_read offsets)
-    const char* kaddr[NS];
-    const char* qaddr[NS];
+    // D = 256: the swizzle only touches chunk bits 0-3, so chunk c + 16 is the address of chunk
+    // c plus 256 bytes: half the address registers (NA of NS), the rest immediate offsets
+    constexpr int NA = HD > 128 ? NS / 2 : NS;
+    constexpr int NTA = HD > 128 ? ND / 2 : ND;
+    const char* kaddr_[NA];
+    const char* qaddr_[NA];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        kaddr[s] = k_lds + lds_off<HD>(wave * kBwdKeysPerWave + lr, 2 * s + hh);   // + 32*ks rows
-        qaddr[s] = q_lds + lds_off<HD>(lr, 2 * s + hh);
+    for (int s = 0; s < NA; ++s) {
+        kaddr_[s] = k_lds + lds_off<HD>(wave * kBwdKeysPerWave + lr, 2 * s + hh);   // + 32*ks rows
+        qaddr_[s] = q_lds + lds_off<HD>(lr, 2 * s + hh);
     }
+    auto kaddr = [&](const int s) { return kaddr_[s % NA] + (s / NA) * 256; };
+    auto qaddr = [&](const int s) { return qaddr_[s % NA] + (s / NA) * 256; };
     const int q4 = (lane & 15) >> 2;
-    int troff[2][ND];   // transposed reads of the Q / dO tile (A operand: rows q, column d)
+    int troff_[2][NTA];   // transposed reads of the Q / dO tile (A operand: rows q, column d)
 #pragma unroll
     for (int part = 0; part < 2; ++part)
 #pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
+        for (int dt = 0; dt < NTA; ++dt) {
             const int r = 4 * hh + q4 + 8 * part;
             const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            troff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            troff_[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
         }
+    auto troff = [&](const int part, const int dt) { return troff_[part][dt % NTA] + (dt / NTA) * 256; };
     // dQ phase (16x16x32): wave -> query half mt, d tiles
     const int mt = wave & 1;
     const int g16 = lane >> 4;
@@ -273,17 +324,36 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     const int qq = (lane & 15) >> 2;
     // tr-read bases for dQ = dS K; the swizzles only see row bits < 4, so the 32-key step
     // is a plain immediate offset (keeps the addresses out of the register budget)
-    int dq_aoff[2], dq_boff[NDQ][2];
+    int dq_aoff[2], dq_boff[HD > 128 ? 1 : NDQ][2];
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
         const int kr0 = 8 * g16 + qq + 4 * part;
         dq_aoff[part] = ds_off(kr0, 16 * mt + 4 * p4);
 #pragma unroll
-        for (int i = 0; i < NDQ; ++i) {
+        for (int i = 0; i < (HD > 128 ? 1 : NDQ); ++i) {
             const int dcol = 16 * ((wave >> 1) * NDQ + i) + 4 * p4;
             dq_boff[i][part] = lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
         }
     }
+
+#if XFA_BWD_DQ32
+    // dS^T tr-read bases for the 32x32x16 dQ product (rows of a 16-key slice, q column quad)
+    int dq32_aoff[2];
+#pragma unroll
+    for (int part = 0; part < 2; ++part)
+        dq32_aoff[part] = ds_off(4 * hh + q4 + 8 * part, 16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+#endif
+
+    // (D > 128: the dQ K-read offsets are recomputed per use instead of held in registers)
+    auto dqb = [&](const int i, const int part) {
+        if constexpr (HD > 128) {
+            const int kr0 = 8 * g16 + qq + 4 * part;
+            const int dcol = 16 * ((wave >> 1) * NDQ + i) + 4 * p4;
+            return lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
+        } else {
+            return dq_boff[i][part];
+        }
+    };
 
     f32x16 dk[KS][ND], dv[KS][ND];
 #pragma unroll
@@ -304,7 +374,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         const int head = hk_i * G + g;
         const int q0 = (t_lo + tt) * BQ;
         const float lsd = lsd_cur;
-        if (it + 1 < n_iter) load_q(it + 1);
+        if (!VR && it + 1 < n_iter) load_q(it + 1);
 
         // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
         f32x16 s_acc[KS], dp_acc[KS];
@@ -312,16 +382,24 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int ks = 0; ks < KS; ++ks) { s_acc[ks] = f32x16{}; dp_acc[ks] = f32x16{}; }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const V8 qa = *reinterpret_cast<const V8*>(qaddr[s]);
-            const V8 ga = *reinterpret_cast<const V8*>(qaddr[s] + QT_BYTES);
+            const V8 qa = *reinterpret_cast<const V8*>(qaddr(s));
+            const V8 ga = *reinterpret_cast<const V8*>(qaddr(s) + QT_BYTES);
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                const V8 kb = *reinterpret_cast<const V8*>(kaddr[s] + ks * 32 * HD * 2);
-                const V8 vb = *reinterpret_cast<const V8*>(kaddr[s] + KT_BYTES + ks * 32 * HD * 2);
+                const V8 kb = *reinterpret_cast<const V8*>(kaddr(s) + ks * 32 * HD * 2);
+                V8 vb;
+                if constexpr (VR) vb = vfrag[s];
+                else vb = *reinterpret_cast<const V8*>(kaddr(s) + KT_BYTES + ks * 32 * HD * 2);
                 s_acc[ks] = DT<T>::mfma32(qa, kb, s_acc[ks]);
                 dp_acc[ks] = DT<T>::mfma32(ga, vb, dp_acc[ks]);
             }
+            // D > 128: keep the scheduler from hoisting every k-step's LDS operands (register
+            // pressure beside the 256 accumulator registers of dK^T / dV^T)
+            if constexpr (HD > 128) __builtin_amdgcn_sched_barrier(0);
         }
+        // (VR: the next tile's Q / dO loads go out only now, so their 32 staging registers are
+        // not live across the S / dP product, the register peak)
+        if (VR && it + 1 < n_iter) load_q(it + 1);
         // ---- P = exp2(S*c - LSE*log2e), dS = P * (dP - D)
         float alibi_w = 0.f;
         if (FEAT && p.alibi) alibi_w = p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul;
@@ -369,11 +447,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             const int rb = 16 * sp * HD * 2;
 #pragma unroll
             for (int dt = 0; dt < ND; ++dt) {
-                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff[0][dt]));
-                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff[1][dt]));
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff(0, dt)));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff(1, dt)));
                 const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff[0][dt]));
-                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff[1][dt]));
+                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff(0, dt)));
+                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff(1, dt)));
                 const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
@@ -383,6 +461,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                     dv[ks][dt] = DT<T>::mfma32(__builtin_bit_cast(V8, av), pb, dv[ks][dt]);
                     dk[ks][dt] = DT<T>::mfma32(__builtin_bit_cast(V8, bv), sb, dk[ks][dt]);
                 }
+                if constexpr (HD > 128) __builtin_amdgcn_sched_barrier(0);
             }
         }
         // ---- dS^T -> LDS (bf16/f16): row = key (this lane), 4 consecutive q per store
@@ -400,6 +479,44 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             }
         }
         __syncthreads();
+#if XFA_BWD_EARLYSTORE
+        // Q / dO of this tile are dead after the barrier above (dQ reads only dS^T and K)
+        if (it + 1 < n_iter) store_q();
+        lsd_cur = lsd_value();      // every vmcnt wait of the iteration comes before its atomics
+        asm volatile("" : "+v"(lsd_cur));   // (pinned: not sunk below the atomics)
+#endif
+#if XFA_BWD_DQ32
+        // ---- dQ[q][32 dt .. +32) += dS K over the 256 keys on v_mfma_f32_32x32x16 by waves
+        // 0..ND-1 (one per SIMD).  A = dS (q on the lane) and B = K (d on the lane) are both
+        // transposing reads of key-row images with the same lane -> (row, column) pattern, so
+        // both carry the same key order.  One accumulator register = two 128-byte row segments
+        // of dQ (rows m, m + 4), the full-rate float-atomic shape (MI355X_MICROARCH.md).
+        static_assert(ND <= NW, "XFA_BWD_DQ32: one 32-column dQ tile per wave");
+        if (wave < ND) {
+            const int dt = wave;
+            f32x16 dq = f32x16{};
+#pragma unroll
+            for (int ks = 0; ks < BN / 16; ++ks) {
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 16 * 64 + dq32_aoff[0]));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 16 * 64 + dq32_aoff[1]));
+                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(k_lds + ks * 16 * HD * 2 + troff(0, dt)));
+                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(k_lds + ks * 16 * HD * 2 + troff(1, dt)));
+                const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                dq = DT<T>::mfma32(__builtin_bit_cast(V8, av), __builtin_bit_cast(V8, bv), dq);
+            }
+            const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+                              (int64_t)(q_off + q0) * p.acc_row;
+            const __amdgpu_buffer_rsrc_t qrs =
+                make_rsrc(qa, (uint32_t)(max(0, sq - q0) * p.acc_row * 4));
+            const int arow = (int)p.acc_row * 4;
+            const int d = 32 * dt + lr;
+            const int base = d < p.d ? (4 * hh) * arow + d * 4 : kOOB;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                dq_atomic_add(dq[r], qrs, base + (8 * (r >> 2) + (r & 3)) * arow);
+        }
+#else
         // ---- dQ[q][d] += dS K over the 256 keys (16x16x32; A = dS via tr-read of dS^T)
         {
             f32x4 dq[NDQ];
@@ -414,12 +531,13 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 #pragma unroll
                 for (int i = 0; i < NDQ; ++i) {
                     const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dq_boff[i][0]));
+                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dqb(i, 0)));
                     const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dq_boff[i][1]));
+                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dqb(i, 1)));
                     const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                     dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
                 }
+                if constexpr (HD > 128) __builtin_amdgcn_sched_barrier(0);
             }
             // buffer atomics over this (batch, head)'s rows [q0, sq): rows past the end and the
             // padded head-dim columns fall outside the descriptor and are dropped (no branches)
@@ -434,11 +552,14 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 const int base = d < p.d ? (16 * mt + 4 * g16) * arow + d * 4 : kOOB;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dq[i][r], qrs, base + r * arow, 0, 0);
+                    dq_atomic_add(dq[i][r], qrs, base + r * arow);
             }
         }
+#endif
+#if !XFA_BWD_EARLYSTORE
         if (it + 1 < n_iter) store_q();
         lsd_cur = lsd_value();
+#endif
         __syncthreads();
     }
 

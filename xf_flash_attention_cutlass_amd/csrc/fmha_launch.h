@@ -40,6 +40,8 @@ hipError_t launch_bwd_hd64_bf16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd64_f16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_bf16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd128_f16(const BwdParams& p, hipStream_t st);
+hipError_t launch_bwd_hd256_bf16(const BwdParams& p, hipStream_t st);
+hipError_t launch_bwd_hd256_f16(const BwdParams& p, hipStream_t st);
 
 // KV-cache append (+ rotary) pass, fmha_append.hip
 struct AppendParams {

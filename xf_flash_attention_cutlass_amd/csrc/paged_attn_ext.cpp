@@ -423,7 +423,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     const int num_heads_k = k.size(2);
     TORCH_CHECK(batch_size > 0, "batch size must be positive");
     TORCH_CHECK(head_size % 8 == 0, "head_size should be a multiple of 8");
-    TORCH_CHECK(head_size <= 128, "this build's backward supports head dimension at most 128");
+    TORCH_CHECK(head_size <= 256, "FlashAttention backward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(head_size == round8(head_size_og), "head_size must be head_size_og rounded to a multiple of 8");
     if (window_size_left >= seqlen_k) window_size_left = -1;
@@ -499,7 +499,8 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     const int total_q = q.size(0), num_heads = q.size(1), head_size = q.size(2);
     const int total_k = k.size(0), num_heads_k = k.size(1);
     const int head_size_og = dout.size(2);
-    TORCH_CHECK(head_size % 8 == 0 && head_size <= 128, "head_size must be a multiple of 8 and <= 128");
+    TORCH_CHECK(head_size % 8 == 0, "head_size should be a multiple of 8");
+    TORCH_CHECK(head_size <= 256, "FlashAttention backward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     if (window_size_left >= max_seqlen_k) window_size_left = -1;
     if (window_size_right >= max_seqlen_k) window_size_right = -1;
