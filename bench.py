@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the fwd_bwd sample")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="name=value tuning option (fmha_set_option) for A/B runs")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed seconds of steps before the warmup (GPU clock ramp)")
     return ap.parse_args()
@@ -137,6 +139,11 @@ def build_workload(a, dev, rank):
     """Returns dict(step, units, bound, config, cpu, out) for the selected mode; `units` is
     the algorithmic FLOPs (mfma-bound) or bytes (hbm-bound) one step processes."""
     import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    for o in a.opt:                       # tuning knobs (fmha_set_option), A/B runs only
+        name, val = o.split("=")
+        if capi.lib().fmha_set_option(name.encode(), int(val)) != 0:
+            raise SystemExit(capi.lib().fmha_last_error().decode())
     pa = xfa.paged_attn
     H, D = a.heads, a.headdim
     causal = not a.no_causal

@@ -517,13 +517,17 @@ def test_fwd_persistent_order_bitexact(xfa, cfg):
     window = cfg.get("window", (-1, -1))
     outs = []
     try:
-        for order in (0, 1):
+        # boustrophedon, XCD-grouped pairs, and the dynamic item queue (twice: the queue's
+        # device counter must have reset itself after the first launch)
+        for order, dyn in ((0, 1), (1, 1), (1, 2), (1, 2)):
             assert L.fmha_set_option(b"fwd_order", order) == 0
+            assert L.fmha_set_option(b"fwd_dyn", dyn) == 0
             o, lse = xfa.flash_attn_func(q, k, v, causal=cfg["causal"], window_size=window,
                                          return_attn_probs=True)[:2]
             outs.append((o.clone(), lse.clone()))
     finally:
         L.fmha_set_option(b"fwd_order", 1)
+        L.fmha_set_option(b"fwd_dyn", 1)
     for o, lse in outs[1:]:
         assert torch.equal(o, outs[0][0])
         assert torch.equal(lse, outs[0][1])
@@ -535,6 +539,35 @@ def test_fwd_persistent_order_bitexact(xfa, cfg):
                                   upcast=False, reorder_ops=True)
         _assert_parity(outs[-1][0][:1, :, :4].float().cpu(), r.cpu(), pt.float().cpu(),
                        what=str(cfg))
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_fwd_varlen_dynamic_queue_bitexact(xfa, causal):
+    """Varlen runs the dynamic item queue by default (fwd_dyn=1): same bits as the static
+    persistent order, launch after launch (the counter resets itself), and the oracle's rule."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(12)
+    h, d = 16, 128
+    lens = [1900, 37, 1024, 1500, 2000, 256, 999, 1777]        # 1024 row-block items > 256 CUs
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    q, k, v = (torch.randn(sum(lens), h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    outs = []
+    try:
+        for dyn in (0, 1, 1, 1):
+            assert L.fmha_set_option(b"fwd_dyn", dyn) == 0
+            o = xfa.flash_attn_varlen_func(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
+            outs.append(o.clone())
+    finally:
+        L.fmha_set_option(b"fwd_dyn", 1)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    for i in (1, 4):                                      # two sequences against the oracle
+        s0, s1 = int(cu[i]), int(cu[i + 1])
+        qs, ks, vs = (x[s0:s1, :4][None].cpu() for x in (q, k, v))
+        r, _ = orc.attention_ref(qs.float(), ks.float(), vs.float(), causal=causal)
+        pt, _ = orc.attention_ref(qs, ks, vs, causal=causal, upcast=False, reorder_ops=True)
+        _assert_parity(outs[-1][s0:s1, :4][None].float().cpu(), r, pt.float(), what=f"seq{i}")
 
 
 # ------------------------------------------------------------------- head dims 129..256 ---

@@ -35,11 +35,22 @@ def main():
     a = ap.parse_args()
 
     from xf_flash_attention_cutlass_amd import capi
-    libs = [capi.load(p) for p in a.libs]
-    for lib in libs:
-        for spec in a.opt:
-            name, val = spec.split("=")
+    # a build may be given as path@name=val,name=val: per-build options (the same .so under
+    # two options is copied to a distinct name so each load has its own option state)
+    import shutil
+    import tempfile
+    libs = []
+    for i, spec in enumerate(a.libs):
+        path, _, opts = spec.partition("@")
+        if opts:
+            tmp = os.path.join(tempfile.mkdtemp(), f"v{i}_" + os.path.basename(path))
+            shutil.copy(path, tmp)
+            path = tmp
+        lib = capi.load(path)
+        for o in a.opt + ([x for x in opts.split(",") if x] if opts else []):
+            name, val = o.split("=")
             assert lib.fmha_set_option(name.encode(), int(val)) == 0, lib.fmha_last_error()
+        libs.append(lib)
     hk = a.hk or a.h
     causal = not a.noncausal
     dt = torch.bfloat16

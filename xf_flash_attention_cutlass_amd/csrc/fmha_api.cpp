@@ -77,6 +77,21 @@ void* pool_get(hipStream_t st, size_t bytes) {
     return e.ptr;
 }
 
+// Item counters of the dynamic persistent forward (one pair of ints per (device, stream),
+// zeroed once; the kernel's last workgroup resets them, so stream order keeps them valid).
+std::map<std::pair<int, hipStream_t>, int*> g_ctr;
+int* counter_get(hipStream_t st) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    int*& c = g_ctr[{dev, st}];
+    if (!c) {
+        if (hipMalloc(&c, 256) != hipSuccess) { c = nullptr; return nullptr; }
+        if (hipMemsetAsync(c, 0, 256, st) != hipSuccess) { (void)hipFree(c); c = nullptr; return nullptr; }
+    }
+    return c;
+}
+
 int g_num_cus = 0;
 int num_cus() {
     if (g_num_cus == 0) {
@@ -203,6 +218,10 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.pipe = options().fwd_pipe;
     p.dbg = options().fwd_dbg;
     p.max_slack = (float)options().fwd_slack;
+    // dynamic item queue: ragged (varlen) row blocks balance across CUs as they finish
+    p.work_ctr = nullptr;
+    const int dyn = options().fwd_dyn;
+    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && p.cu_seqlens_q))) p.work_ctr = counter_get(st);
     options().num_cus = num_cus();
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
@@ -235,6 +254,7 @@ int fmha_set_option(const char* name, int value) {
         return 0;
     }
     if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_decode16")) { options().fwd_decode16 = value ? 1 : 0; return 0; }

@@ -72,7 +72,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         const int items = p.b * p.hk * n_mb;
         const int slots = options().num_cus * options().fwd_persistent;
         if (items > slots) {
-            pp.persistent = (options().fwd_order == 1 && slots % 8 == 0) ? 2 : 1;
+            pp.persistent = p.work_ctr ? 3 : (options().fwd_order == 1 && slots % 8 == 0) ? 2 : 1;
             grid = dim3(slots, 1, grid.z);
         }
     }

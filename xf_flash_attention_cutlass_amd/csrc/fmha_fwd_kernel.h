@@ -621,6 +621,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
 template <int HD, typename T, int NW, bool MASK, bool FEAT>
 __global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int s_claim[2];
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
     for (int k = 0;; ++k) {        // one call site: the item body is inlined once
@@ -638,6 +639,16 @@ __global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kern
             const int i = q - bh * npair;
             m_block = (k & 1) ? i : nm - 1 - i;
             if ((k & 1) && i == nm - 1 - i) continue;   // odd count: the middle block is alone
+        } else if (p.persistent == 3) {
+            // dynamic queue: claim the next item (heaviest row block first, then (b, kv head))
+            // from a device counter, so ragged varlen items balance as workgroups finish; the
+            // claim slot alternates so a fast wave's next claim cannot overwrite it unread
+            if (threadIdx.x == 0) s_claim[k & 1] = atomicAdd(p.work_ctr, 1);
+            __syncthreads();
+            const int q = s_claim[k & 1];
+            if (q >= nbh * p.n_mblocks) break;
+            bh = q % nbh;
+            m_block = p.n_mblocks - 1 - q / nbh;
         } else if (p.persistent) {
             const int lin = k * g + ((k & 1) ? g - 1 - (int)blockIdx.x : (int)blockIdx.x);
             if (lin >= nbh * p.n_mblocks) break;
@@ -649,6 +660,15 @@ __global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kern
             m_block = gridDim.y - 1 - blockIdx.y;
         }
         fwd_item<HD, T, NW, MASK, FEAT>(p, smem, bh, m_block, blockIdx.z);
+    }
+    // dynamic queue: every workgroup has made its last (failed) claim when it gets here; the
+    // last one to finish resets the counters for the next launch on this stream
+    if (p.persistent == 3 && threadIdx.x == 0) {
+        const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+        if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {
+            atomicExch(p.work_ctr, 0);
+            atomicExch(p.work_ctr + 1, 0);
+        }
     }
 }
 
