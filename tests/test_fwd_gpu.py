@@ -554,7 +554,7 @@ def test_fwd_varlen_dynamic_queue_bitexact(xfa, causal):
     q, k, v = (torch.randn(sum(lens), h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
     outs = []
     try:
-        for dyn in (0, 1, 1, 1):
+        for dyn in (0, 1, 1, 3, 3):
             assert L.fmha_set_option(b"fwd_dyn", dyn) == 0
             o = xfa.flash_attn_varlen_func(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
             outs.append(o.clone())

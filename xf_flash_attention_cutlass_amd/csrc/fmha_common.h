@@ -98,7 +98,8 @@ struct FwdParams {
     float max_slack;           // log2 units the running max may lag the true max before the
                                // O / l rescale (deferred rescale; 0 = rescale on every rise)
     int decode;                // 1: run fmha_decode_kernel (split-KV decode)
-    int* work_ctr;             // persistent == 3: self-resetting item counter [next, finished]
+    int* work_ctr;             // persistent == 3: self-resetting counters [-, finished, next x 8]
+    int xcd_queues;            // persistent == 3: one item queue per XCD (else queue 0 only)
 };
 
 struct CombineParams {
