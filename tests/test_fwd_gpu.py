@@ -519,15 +519,17 @@ def test_fwd_persistent_order_bitexact(xfa, cfg):
     try:
         # boustrophedon, XCD-grouped pairs, and the dynamic item queue (twice: the queue's
         # device counter must have reset itself after the first launch)
-        for order, dyn in ((0, 1), (1, 1), (1, 2), (1, 2)):
+        for order, dyn, xq in ((0, 1, 1), (1, 1, 1), (1, 2, 1), (1, 2, 1), (1, 2, 0)):
             assert L.fmha_set_option(b"fwd_order", order) == 0
             assert L.fmha_set_option(b"fwd_dyn", dyn) == 0
+            assert L.fmha_set_option(b"fwd_xcdq", xq) == 0
             o, lse = xfa.flash_attn_func(q, k, v, causal=cfg["causal"], window_size=window,
                                          return_attn_probs=True)[:2]
             outs.append((o.clone(), lse.clone()))
     finally:
         L.fmha_set_option(b"fwd_order", 1)
         L.fmha_set_option(b"fwd_dyn", 1)
+        L.fmha_set_option(b"fwd_xcdq", 1)
     for o, lse in outs[1:]:
         assert torch.equal(o, outs[0][0])
         assert torch.equal(lse, outs[0][1])
@@ -554,12 +556,14 @@ def test_fwd_varlen_dynamic_queue_bitexact(xfa, causal):
     q, k, v = (torch.randn(sum(lens), h, d, device=DEV, dtype=torch.bfloat16) for _ in range(3))
     outs = []
     try:
-        for dyn in (0, 1, 1, 3, 3):
+        for dyn, xq in ((0, 1), (1, 1), (1, 1), (1, 0), (1, 0)):
             assert L.fmha_set_option(b"fwd_dyn", dyn) == 0
+            assert L.fmha_set_option(b"fwd_xcdq", xq) == 0
             o = xfa.flash_attn_varlen_func(q, k, v, cu, cu, max(lens), max(lens), causal=causal)
             outs.append(o.clone())
     finally:
         L.fmha_set_option(b"fwd_dyn", 1)
+        L.fmha_set_option(b"fwd_xcdq", 1)
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     for i in (1, 4):                                      # two sequences against the oracle

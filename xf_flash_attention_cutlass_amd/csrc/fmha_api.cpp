@@ -221,8 +221,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     // dynamic item queue: ragged (varlen) row blocks balance across CUs as they finish
     p.work_ctr = nullptr;
     const int dyn = options().fwd_dyn;
-    if (!p.decode && splits == 1 && (dyn == 2 || ((dyn == 1 || dyn == 3) && p.cu_seqlens_q)))
-        p.work_ctr = counter_get(st);
+    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && p.cu_seqlens_q))) p.work_ctr = counter_get(st);
     options().num_cus = num_cus();
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
@@ -255,7 +254,8 @@ int fmha_set_option(const char* name, int value) {
         return 0;
     }
     if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 3 ? 3 : value); return 0; }
+    if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
+    if (!strcmp(name, "fwd_xcdq")) { options().fwd_xcdq = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_decode16")) { options().fwd_decode16 = value ? 1 : 0; return 0; }

@@ -73,7 +73,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         const int slots = options().num_cus * options().fwd_persistent;
         if (items > slots) {
             pp.persistent = p.work_ctr ? 3 : (options().fwd_order == 1 && slots % 8 == 0) ? 2 : 1;
-            pp.xcd_queues = p.work_ctr && options().fwd_dyn == 3 && slots % 8 == 0 && p.b * p.hk >= 8;
+            pp.xcd_queues = p.work_ctr && options().fwd_xcdq && slots % 8 == 0 && p.b * p.hk >= 8;
             grid = dim3(slots, 1, grid.z);
         }
     }

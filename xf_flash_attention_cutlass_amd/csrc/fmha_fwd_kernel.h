@@ -643,17 +643,22 @@ __global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kern
             // dynamic queue: claim the next item (heaviest row block first, then (b, kv head))
             // from a device counter, so ragged varlen items balance as workgroups finish; the
             // claim slot alternates so a fast wave's next claim cannot overwrite it unread
-            // fwd_dyn=3 (p.xcd_queues): one queue per XCD over the units bh = x (mod 8), so a
-            // unit's row blocks run on one XCD and share its L2 for K/V (workgroup b sits on
-            // XCD b % 8; slots % 8 == 0 and nbh >= 8 are checked on the host)
+            // p.xcd_queues (default): one queue per XCD over the units bh = x (mod 8), unit-major,
+            // so a unit's row blocks run together on one XCD and share its L2 for K/V (workgroup
+            // b sits on XCD b % 8; slots % 8 == 0 and nbh >= 8 are checked on the host)
             const int x = p.xcd_queues ? (int)(blockIdx.x & 7) : 0;
             const int nq = p.xcd_queues ? (nbh - x + 7) >> 3 : nbh;
             if (threadIdx.x == 0) s_claim[k & 1] = atomicAdd(p.work_ctr + 2 + x, 1);
             __syncthreads();
             const int q = s_claim[k & 1];
             if (q >= nq * p.n_mblocks) break;
-            bh = p.xcd_queues ? x + 8 * (q % nq) : q % nq;
-            m_block = p.n_mblocks - 1 - q / nq;
+            if (p.xcd_queues) {     // unit-major: an XCD's workgroups share a unit's K/V in L2
+                bh = x + 8 * (q / p.n_mblocks);
+                m_block = p.n_mblocks - 1 - q % p.n_mblocks;
+            } else {                // heaviest row block first over all units
+                bh = q % nq;
+                m_block = p.n_mblocks - 1 - q / nq;
+            }
         } else if (p.persistent) {
             const int lin = k * g + ((k & 1) ? g - 1 - (int)blockIdx.x : (int)blockIdx.x);
             if (lin >= nbh * p.n_mblocks) break;

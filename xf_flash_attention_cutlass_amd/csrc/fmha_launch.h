@@ -19,6 +19,8 @@ struct Options {
     int fwd_slack = 8;        // deferred rescale: running max may lag by this many log2 units
     int fwd_order = 1;        // persistent item order: 0 boustrophedon, 1 XCD-grouped pairs
     int fwd_dyn = 1;          // dynamic item queue: 0 never, 1 varlen only, 2 every persistent launch
+    int fwd_xcdq = 1;         // dynamic queue kind: 1 one unit-major queue per XCD, 0 one global
+                              // heaviest-row-block-first queue
     int fwd_pipe = 1;         // software-pipelined loop over the unmasked key tiles
     int fwd_dbg = 0;          // timing experiments only (results invalid when set)
     int fwd_decode = 1;       // split-KV decode kernel when seqlen_q * H/Hk <= 32
