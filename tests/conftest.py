@@ -21,3 +21,16 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _tuning_options():
+    """XFA_TEST_OPTIONS="name=value,..." runs the suite under fmha_set_option knobs (A/B builds
+    and schedules get the same parity coverage as the defaults)."""
+    spec = os.environ.get("XFA_TEST_OPTIONS", "")
+    if spec:
+        from xf_flash_attention_cutlass_amd import capi
+        for o in spec.split(","):
+            name, val = o.split("=")
+            assert capi.lib().fmha_set_option(name.encode(), int(val)) == 0, name
+    yield
