@@ -191,7 +191,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         const int tiles = (p.seqlen_k + 31) / 32;
         const int work = p.b * p.hk;
         int zs = num_splits_req > 0 ? (num_splits_req + 3) / 4
-                                    : (2 * num_cus() + work - 1) / work;
+                                    : (options().dec_wg_per_cu * num_cus() + work - 1) / work;
         zs = std::max(1, std::min(zs, std::max(1, tiles / 8)));
         zs = std::min(zs, 32);
         splits = 4 * zs;
@@ -256,6 +256,11 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
     if (!strcmp(name, "fwd_xcdq")) { options().fwd_xcdq = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "dec_wg_per_cu")) {
+        if (value < 1 || value > 16) { fail(1, "dec_wg_per_cu must be in [1, 16]"); return -1; }
+        options().dec_wg_per_cu = value;
+        return 0;
+    }
     if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
     if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_decode16")) { options().fwd_decode16 = value ? 1 : 0; return 0; }
