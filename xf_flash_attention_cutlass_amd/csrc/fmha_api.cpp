@@ -256,6 +256,7 @@ int fmha_set_option(const char* name, int value) {
     if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
     if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
     if (!strcmp(name, "fwd_xcdq")) { options().fwd_xcdq = value ? 1 : 0; return 0; }
+    if (!strcmp(name, "bwd_prio")) { options().bwd_prio = value ? 1 : 0; return 0; }
     if (!strcmp(name, "dec_wg_per_cu")) {
         if (value < 1 || value > 16) { fail(1, "dec_wg_per_cu must be in [1, 16]"); return -1; }
         options().dec_wg_per_cu = value;
@@ -497,6 +498,7 @@ static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl,
     p.scale = softmax_scale;
     p.scale_log2 = scale_softmax * 1.4426950408889634f;
     p.alibi_mul = 1.f / scale_softmax;
+    p.prio_hi = options().bwd_prio;
     return true;
 }
 

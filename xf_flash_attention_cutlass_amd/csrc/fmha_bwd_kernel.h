@@ -362,6 +362,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
+    if (p.prio_hi && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     float lsd_cur = 0.f;
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible

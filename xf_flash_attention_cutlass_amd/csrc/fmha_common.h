@@ -145,6 +145,7 @@ struct BwdParams {
     float softcap_pre;
     float alibi_mul;
     int softcap_on;
+    int prio_hi;         // 1: waves NW/2.. run at s_setprio 1 (A/B knob)
 };
 
 // ------------------------------------------------------------------ dtype traits --

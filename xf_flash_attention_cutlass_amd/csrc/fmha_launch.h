@@ -24,6 +24,7 @@ struct Options {
     int fwd_pipe = 1;         // software-pipelined loop over the unmasked key tiles
     int fwd_dbg = 0;          // timing experiments only (results invalid when set)
     int fwd_decode = 1;       // split-KV decode kernel when seqlen_q * H/Hk <= 32
+    int bwd_prio = 0;         // backward: static s_setprio 1 for the younger half (A/B)
     int dec_wg_per_cu = 2;    // decode split target: workgroups per CU over all (b, kv head)
     int fwd_decode16 = 0;     // 16x16x32 decode tile when seqlen_q * H/Hk <= 16 (slower on C5: A/B knob)
     int num_cus = 256;        // filled by the C ABI from the device
