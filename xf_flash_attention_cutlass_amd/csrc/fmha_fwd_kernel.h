@@ -217,7 +217,9 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     f32x16 acc_o[ND];
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) acc_o[dt] = f32x16{};
-    float m_run = -INFINITY;
+    // running row max in scaled (log2) units: P = exp2(S c - m_sc); -inf until the row's first
+    // visible key
+    float m_sc = -INFINITY;
     float l_run = 0.f;
 
     // ---- the pieces of one 64-key tile
@@ -248,21 +250,22 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             if (need_mask && (key >= my_lr || key < my_ll)) st[kt][r] = -INFINITY;
         }
     };
-    // Deferred rescale: the running max m_run (the exp reference) only moves once some row's
-    // true max exceeds it by more than max_slack (log2 units), so P = exp2(S c - m_run c) stays
-    // below 2^max_slack; O, l and the LSE are all relative to the same m_run, so the result is
+    // Deferred rescale: the running max m_sc (the exp reference) only moves once some row's
+    // true max exceeds it by more than max_slack (log2 units), so P = exp2(S c - m_sc) stays
+    // below 2^max_slack; O, l and the LSE are all relative to the same m_sc, so the result is
     // unchanged up to rounding (the relative rounding of P in T does not depend on the scale).
+    auto rescale_o = [&](const float alpha) {
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+    };
     auto raise_max = [&](const float mx) {
-        const float m_new = fmaxf(m_run, mx);
-        if (__any(m_new * c > m_run * c + p.max_slack)) {
-            const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
-            const float alpha = fast_exp2(m_run * c - mref);
-            l_run *= alpha;
-#pragma unroll
-            for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
-            m_run = m_new;
+        const float m_new = fmaxf(m_sc, mx * c);
+        if (__any(m_new > m_sc + p.max_slack)) {
+            rescale_o(m_new == -INFINITY ? 1.f : fast_exp2(m_sc - m_new));
+            m_sc = m_new;
         }
     };
     // P = exp2(S c - m c) -> T (the B operand of the PV product) for values [v0, v0 + n);
@@ -285,7 +288,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         }
     };
     auto exp_ref = [&]() {
-        const float mref = (m_run == -INFINITY) ? 0.f : m_run * c;
+        const float mref = (m_sc == -INFINITY) ? 0.f : m_sc;
         return f2{mref, mref};
     };
     // S^T = K Q^T (LDS reads one k-step ahead of the MFMAs)
@@ -327,6 +330,39 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         float rs[2] = {0.f, 0.f};
         exp_part(st, pb, exp_ref(), rs, 0, 32);
         l_run += rs[0] + rs[1];
+    };
+    // The pipeline's scores are X = S c - m_sc already: P = exp2(X) -> T for values [v0, v0 + n)
+    auto expx_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], const int v0, const int n) {
+#pragma unroll
+        for (int v = v0; v < v0 + n; v += 2) {
+            const int kt = v >> 4, r = v & 15;
+            const T2 e = {(T)fast_exp2(st[kt][r]), (T)fast_exp2(st[kt][r + 1])};
+            pb[2 * kt + (r >> 3)][r & 7] = e[0];
+            pb[2 * kt + (r >> 3)][(r & 7) + 1] = e[1];
+        }
+    };
+    auto expx_tile = [&](const f32x16 (&st)[2], V8 (&pb)[4]) {
+        expx_part(st, pb, 0, 32);
+        float rs = 0.f;
+#pragma unroll
+        for (int pi = 0; pi < 16; ++pi)
+            rs = DT<T>::sum2(T2{pb[pi >> 2][2 * (pi & 3)], pb[pi >> 2][2 * (pi & 3) + 1]}, rs);
+        l_run += rs;
+    };
+    // Deferred rescale on pipeline scores: mx = this row's max of X = S c - m_sc over the new
+    // tile.  Rows still at m_sc = -inf had X computed against 0 (exp_ref) and take m_sc = mx.
+    auto rescale_x = [&](const float mx, f32x16 (&sx)[2]) {
+        const bool fresh = m_sc == -INFINITY;
+        if (__any(mx > p.max_slack || (fresh && mx != -INFINITY))) {
+            // a volatile asm cannot be speculated: keeps the rare rescale a real branch
+            // (if-converted it costs 64 VALU on every tile)
+            asm volatile("; rescale_x");
+            const float delta = fresh ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
+            rescale_o(fresh ? 1.f : fast_exp2(-delta));
+#pragma unroll
+            for (int v = 0; v < 32; ++v) sx[v >> 4][v & 15] -= delta;
+            m_sc = fresh ? (mx == -INFINITY ? -INFINITY : mx) : m_sc + delta;
+        }
     };
 
     // ---- tiles that need per-wave masking / skipping: one tile in flight, two LDS buffers
@@ -457,7 +493,14 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // Tiles [lo, hm) need no mask; tiles [hm, hi) (the causal diagonal / right window edge /
     // ragged end) are masked in registers on the way through the same pipeline (a wave whose
     // rows cannot see such a tile computes zeros for it instead of branching out of the
-    // interleaved schedule).
+    // interleaved schedule).  Every row sees tile lo (f_lo lies past every row's left window
+    // edge, and visible keys are contiguous), so only the right edge can cut a pipeline tile.
+    //
+    // Scores leave phase b already scaled and shifted, X = S c - m_sc, so phase a is exp + cvt
+    // only; the VALU of a tile splits evenly between the two MFMA phases (per wave and tile:
+    // a = 32 v_exp + 16 cvt beside 16 QK^T MFMAs, b = 32 fma + 16 max3 + 16 dot2c row sums beside
+    // 16 PV MFMAs), each within the MFMA gaps.  The edge mask runs after phase b on the edge tiles only.
+    const int lim_e = my_lr - 4 * hh;            // right edge of this lane's keys, minus its offset
     auto pipe_range = [&](const int lo, const int hm, const int hi) {
         const bool third = lo + 2 < hi;
         dma_tile(lo, 0);
@@ -470,18 +513,21 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         qk(0, sa);
         transform_part(sa, lo * kBlockN, lo >= hm, 0, 32);
         raise_max(row_max(sa));
+        {
+            const float mr = exp_ref()[0];
+#pragma unroll
+            for (int v = 0; v < 32; ++v) sa[v >> 4][v & 15] = __builtin_fmaf(sa[v >> 4][v & 15], c, -mr);
+        }
         const int nsteps = hi - lo - 1;
         auto step = [&](auto KB, auto VB, auto WB, const int j, f32x16 (&st)[2], f32x16 (&sn)[2]) {
             constexpr int ks = decltype(KB)::value, vs = decltype(VB)::value, wb = decltype(WB)::value;
             const bool issue = j + 3 < hi;
             if (issue) dma_tile(j + 3, wb);
             if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
-            // phase a: S_{j+1} = K_{j+1} Q^T on the MFMA pipe, P_j = exp(S_j) on the VALU
+            // phase a: S_{j+1} = K_{j+1} Q^T on the MFMA pipe, P_j = exp2(X_j) -> T on the VALU
             sn[0] = f32x16{};
             sn[1] = f32x16{};
             V8 pb[4];
-            const f2 m2 = exp_ref();
-            float rs[2] = {0.f, 0.f};
             constexpr int EV = 32 / (2 * NS);     // exp values per QK^T MFMA
             V8 a0 = rd_k(ks, 0, 0), a1 = rd_k(ks, 0, 1);
 #pragma unroll
@@ -489,22 +535,24 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 V8 n0 = a0, n1 = a1;
                 if (s + 1 < NS) { n0 = rd_k(ks, s + 1, 0); n1 = rd_k(ks, s + 1, 1); }
                 sn[0] = DT<T>::mfma32(a0, qf[s], sn[0]);
-                exp_part(st, pb, m2, rs, (2 * s) * EV, EV);
+                expx_part(st, pb, (2 * s) * EV, EV);
                 sn[1] = DT<T>::mfma32(a1, qf[s], sn[1]);
-                exp_part(st, pb, m2, rs, (2 * s + 1) * EV, EV);
+                expx_part(st, pb, (2 * s + 1) * EV, EV);
                 a0 = n0;
                 a1 = n1;
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             }
-            l_run += rs[0] + rs[1];
-            // phase b: O += V_j^T P_j on the MFMA pipe, transform + row max of S_{j+1} on the
-            // VALU; V^T read two MFMAs ahead (asm reads, explicit lgkmcnt)
+            // phase b: O += V_j^T P_j on the MFMA pipe; on the VALU X_{j+1} = S_{j+1} c - m_sc
+            // (transforms and edge mask first), its row max, and the row sum of P_j; V^T read
+            // two MFMAs ahead (asm reads, explicit lgkmcnt)
             constexpr int MV = 32 / NPV;          // score values per PV MFMA
             auto voffs = [&](auto I) {             // immediate offset of PV operand I
                 constexpr int i = decltype(I)::value;
                 return std::integral_constant<int, vs * TILE + (32 * (i / (2 * ND)) + 16 * ((i / ND) & 1)) * HD * 2>{};
             };
+            const float mr = exp_ref()[0];
             float mx = -INFINITY;
+            float rs = 0.f;
             V8 ring[3];
             ring[0] = rd_v_asm(voffs(std::integral_constant<int, 0>{}), 0);
             ring[1] = rd_v_asm(voffs(std::integral_constant<int, 1>{}), 1 % ND);
@@ -521,21 +569,39 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 acc_o[i % ND] = DT<T>::mfma32(ring[i % 3], pb[i / ND], acc_o[i % ND]);
                 if (FEAT) transform_part(sn, (j + 1) * kBlockN, false, i * MV, MV);
 #pragma unroll
-                for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
+                for (int v = i * MV; v < (i + 1) * MV; ++v)
+                    sn[v >> 4][v & 15] = __builtin_fmaf(sn[v >> 4][v & 15], c, -mr);
+                if constexpr (MV == 2) mx = fmaxf(fmaxf(mx, sn[(i * 2) >> 4][(i * 2) & 15]), sn[(i * 2 + 1) >> 4][(i * 2 + 1) & 15]);
+                else {
+#pragma unroll
+                    for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
+                }
+                // row sum of the rounded P_j weights (the normaliser is exactly the sum of the
+                // weights the PV MFMA multiplies): 16 pairs over the NPV MFMAs
+                constexpr int PPM = 16 / NPV;     // P pairs per PV MFMA
+#pragma unroll
+                for (int u = 0; u < PPM; ++u) {
+                    const int pi = i * PPM + u;
+                    rs = DT<T>::sum2(T2{pb[pi >> 2][2 * (pi & 3)], pb[pi >> 2][2 * (pi & 3) + 1]}, rs);
+                }
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             });
-            if (j + 1 >= hm) {                    // edge tile: mask after the transforms
-                const int n0 = (j + 1) * kBlockN + 4 * hh;
+            // opaque uses pin the row sum and the max chain inside phase b (else they are sunk
+            // below the edge branch, out of the MFMA gaps)
+            asm volatile("" : "+v"(rs), "+v"(mx));
+            l_run += rs;
+            if (j + 1 >= hm) {                    // edge tile: mask, then the row max again
+                const int lim_t = lim_e - (j + 1) * kBlockN;
+                float mm = -INFINITY;
 #pragma unroll
                 for (int v = 0; v < 32; ++v) {
-                    const int key = n0 + 32 * (v >> 4) + (v & 3) + 8 * ((v & 15) >> 2);
-                    if (key >= my_lr || key < my_ll) sn[v >> 4][v & 15] = -INFINITY;
+                    const int off = 32 * (v >> 4) + ((v & 15) & 3) + 8 * ((v & 15) >> 2);
+                    if (off >= lim_t) sn[v >> 4][v & 15] = -INFINITY;
+                    mm = fmaxf(mm, sn[v >> 4][v & 15]);
                 }
-                mx = sn[0][0];
-#pragma unroll
-                for (int v = 1; v < 32; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
+                mx = mm;
             }
-            raise_max(wave_max_halves(mx));
+            rescale_x(wave_max_halves(mx), sn);
             publish(issue);                       // tile j+2 landed everywhere
         };
         typedef std::integral_constant<int, 0> I0;
@@ -556,12 +622,11 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         }
         // drain: the last tile's softmax and PV
         V8 pb[4];
-        if (nsteps & 1) exp_tile(sb, pb);
-        else exp_tile(sa, pb);
+        if (nsteps & 1) expx_tile(sb, pb);
+        else expx_tile(sa, pb);
         pv(nsteps & 3, pb);
         __syncthreads();
     };
-
     // Key tiles: [nb_lo, f_lo) cross the left window edge (per-wave masked loop);
     // [f_lo, f_hi) every row of the workgroup sees in full; [f_hi, nb_hi) cross the right
     // window edge / the end of the keys.  The last two ranges run through the pipeline.
@@ -599,7 +664,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                            acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv};
                 *reinterpret_cast<f32x4*>(oa + d) = v;
             }
-        if (hh == 0) p.lseaccum[rid] = empty ? -INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+        if (hh == 0) p.lseaccum[rid] = empty ? -INFINITY : (m_sc + __log2f(l_full)) * kLn2;
         return;
     }
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
@@ -609,7 +674,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     else store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
     if (p.lse && hh == 0) {
         p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] =
-            empty ? INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+            empty ? INFINITY : (m_sc + __log2f(l_full)) * kLn2;
     }
 }
 
