@@ -83,13 +83,23 @@ const char* fmha_last_error(void);
 /* 0 if the last call on this thread succeeded, a nonzero code otherwise. */
 int fmha_last_status(void);
 
+/* KV split count the last forward call on this thread launched with (1 = single pass; decode
+ * kernel: one split per wave).  Diagnostic, for tests and tuning. */
+int fmha_last_num_splits(void);
+
 /* Library version / build identification, e.g. "xf-fmha-gfx950 1.0". */
 const char* fmha_version(void);
 
-/* Process-wide tuning knobs (not thread-safe against concurrent launches).  Returns 0, or -1
- * for an unknown name / invalid value.  "fwd_waves": 4 or 8 waves (128 / 256 query rows) per
- * forward workgroup. */
+/* Process-wide schedule knobs; every setting computes the same results (the parity suite runs
+ * under any of them).  Each knob is an atomic value read once per call, so setting one while
+ * another thread launches is safe (that launch sees the old or the new value).  Returns 0, or
+ * -1 for an unknown name / out-of-range value.  Knobs: fwd_waves (4 | 8 waves = 128 | 256
+ * query rows per forward workgroup), fwd_prio (0/1), fwd_persistent (workgroups per CU, 0 =
+ * one workgroup per item), fwd_slack (0..16), fwd_order (0/1), fwd_dyn (0..2), fwd_xcdq (0/1),
+ * fwd_pipe (0..2), fwd_decode (0/1), dec_wg_per_cu (1..16). */
 int fmha_set_option(const char* name, int value);
+/* Current value of a knob, or -1 (with fmha_last_error set) for an unknown name. */
+int fmha_get_option(const char* name);
 
 /* Varlen forward with the fields the reference's varlen C entry drops (paged_attn.cpp:423-433):
  * LSE out (fp32 [num_heads, total_q], unpadded as export.cpp:827; total_q = cu_seqlens_q[batch]
@@ -129,6 +139,9 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
  * rotary_sin: [seqlen_ro, rotary_dim / 2] in q's dtype; interleaved = GPT-J pairs (2i, 2i+1),
  * else GPT-NeoX halves (i, i + rotary_dim/2).  knew/vnew contiguous [b, seqlen_new, hk, d];
  * caches contiguous [num_blocks, page, hk, d]; q/q_out contiguous [b, seqlen_q, h, d].
+ * seqlens_out must be a different buffer from cache_seqlens (rejected otherwise: the kernel
+ * reads the old lengths while writing the new ones).  New rows whose slot falls past the
+ * block table's row (pos >= block_table_stride * page) are dropped.
  * Stream-ordered; run the attention (fmha_page_kvcache_fwd_ex with seqlens_out) after it. */
 void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const void* knew,
                          const void* vnew, int32_t seqlen_new, const void* block_table,
@@ -144,7 +157,12 @@ void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const
  * softmax_lse fp32 [batch, heads, seqlen_q] from fmha_fwd; outputs dq [b,sq,h,d],
  * dk/dv [b,sk,hk,d] (GQA groups reduced in-kernel, no host sum_out), softmax_d fp32
  * [batch, heads, seqlen_q] (may be NULL: then pool scratch is used).
- * workspace: optional caller scratch of fmha_bwd_workspace_size() bytes; NULL = pool. */
+ * deterministic: dQ partials of each key block go to their own fp32 slice and are summed in
+ * key-block order (bitwise reproducible; export.cpp:1086-1092 splits dq_accum the same way),
+ * instead of float atomics into one accumulator.
+ * workspace: optional caller scratch of fmha_bwd_workspace_size(..., deterministic) bytes;
+ * NULL = pool.  One sequence's slab of any tensor must stay under 2 GiB - 256 bytes (32-bit
+ * buffer offsets); larger inputs fail with an error, never a wrong result. */
 void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
               void* dq, void* dk, void* dv, void* alibi_slopes, void* softmax_d,
               int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
@@ -153,21 +171,26 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
               bool is_fp16, hipStream_t stream, void* workspace, size_t workspace_bytes);
 
 size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
-                               int32_t num_heads, int32_t num_heads_k, int32_t head_size);
+                               int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                               bool deterministic);
 
 /* Varlen backward (mha_varlen_bwd semantics, flash_api_hip.cpp:1045-1298): packed q/k/v/out/
- * dout, cu_seqlens int32 [batch+1], softmax_lse fp32 [num_heads, total_q]. */
+ * dout, cu_seqlens int32 [batch+1], softmax_lse fp32 [num_heads, total_q]; softmax_d fp32
+ * [num_heads, total_q] receives rowsum(dO*O) (may be NULL: pool scratch).  deterministic and
+ * workspace as fmha_bwd (fmha_varlen_bwd_workspace_size(..., deterministic) bytes). */
 void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
                      void* dq, void* dk, void* dv, void* cu_seqlens_q, void* cu_seqlens_k,
                      void* alibi_slopes, int32_t alibi_batch_stride, int32_t max_seqlen_q,
                      int32_t max_seqlen_k, int32_t total_q, int32_t total_k,
                      int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
                      int32_t head_size, float softmax_scale, int window_size_left,
-                     int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
-                     void* workspace, size_t workspace_bytes);
+                     int window_size_right, float softcap, bool deterministic, bool is_fp16,
+                     hipStream_t stream, void* workspace, size_t workspace_bytes,
+                     void* softmax_d);
 
-size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t total_k, int32_t batch_size,
-                                      int32_t num_heads, int32_t num_heads_k, int32_t head_size);
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t batch_size,
+                                      int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                                      bool deterministic);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -34,3 +34,19 @@ def _tuning_options():
             name, val = o.split("=")
             assert capi.lib().fmha_set_option(name.encode(), int(val)) == 0, name
     yield
+
+
+_REPORT = []
+
+
+@pytest.fixture(scope="session")
+def parity_report():
+    """Collects {case, metric, err, bound} rows; XFA_PARITY_REPORT=<path> writes them as JSON
+    at the end of the session (the committed profiles/r*_parity.json evidence)."""
+    yield _REPORT.append
+    path = os.environ.get("XFA_PARITY_REPORT")
+    if path and _REPORT:
+        import json
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(_REPORT, f, indent=1)

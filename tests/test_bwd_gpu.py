@@ -128,7 +128,8 @@ def test_bwd_capi_workspace_and_errors(xfa):
     out, lse = xfa.paged_attn.fwd(q, q, q, None, None, 0.0, d ** -0.5, True, -1, -1, 0.0,
                                   False, None)[0::5][:2]
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
-    ws_n = L.fmha_bwd_workspace_size(s, s, b, h, h, d)
+    ws_n = L.fmha_bwd_workspace_size(s, s, b, h, h, d, False)
+    assert L.fmha_bwd_workspace_size(s, 1000, b, h, h, d, True) > ws_n
     ws = torch.empty(ws_n, device=DEV, dtype=torch.uint8)
     args = [q.data_ptr()] * 4 + [out.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(),
                                  dv.data_ptr(), None, None, s, s, b, h, h, d, 0.0, d ** -0.5, -1,
@@ -137,6 +138,70 @@ def test_bwd_capi_workspace_and_errors(xfa):
     capi.check()
     L.fmha_bwd(*args, ws.data_ptr(), 16)
     assert L.fmha_last_status() != 0 and "workspace" in L.fmha_last_error().decode()
+    # deterministic: one dq_accum slice per 256-key block (a single block here)
+    assert L.fmha_bwd_workspace_size(s, s, b, h, h, d, True) == ws_n
+    args_det = list(args)
+    args_det[22] = True
+    L.fmha_bwd(*args_det, ws.data_ptr(), ws_n)
+    capi.check()
+
+
+def _run_det(xfa, q, k, v, g, **kw):
+    return _run(xfa, q, k, v, g, deterministic=True, **kw)
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("causal,window", [(False, (-1, -1)), (True, (-1, -1)), (False, (100, 30))])
+@pytest.mark.parametrize("sq,sk,h,hk", [(700, 700, 4, 2), (300, 1100, 2, 1)])
+def test_bwd_deterministic(xfa, d, causal, window, sq, sk, h, hk):
+    """deterministic=True (export.cpp:1086-1092 semantics): dQ partials per key block are summed
+    in key-block order, so two runs agree bit for bit; the gradients meet the oracle rule and
+    equal the atomic path's to fp32 reassociation."""
+    gen = torch.Generator().manual_seed(11)
+    q = torch.randn(2, sq, h, d, generator=gen).bfloat16()
+    k = torch.randn(2, sk, hk, d, generator=gen).bfloat16()
+    v = torch.randn(2, sk, hk, d, generator=gen).bfloat16()
+    g = torch.randn(2, sq, h, d, generator=gen).bfloat16()
+    a = _run_det(xfa, q, k, v, g, causal=causal, window_size=window)
+    b_ = _run_det(xfa, q, k, v, g, causal=causal, window_size=window)
+    for x, y in zip(a, b_):
+        assert torch.equal(x, y)
+    nondet = _run(xfa, q, k, v, g, causal=causal, window_size=window)
+    assert torch.equal(a[1], nondet[1]) and torch.equal(a[2], nondet[2])   # dK/dV: no atomics
+    assert (a[0].float() - nondet[0].float()).abs().max().item() < 2e-2
+    w = (window[0], sk) if window[0] >= 0 and window[1] < 0 else window
+    ref, pt = _oracle_grads(q, k, v, g, causal=causal, window_size=w)
+    for nm, x, r, p in zip(("dq", "dk", "dv"), a, ref, pt):
+        _grad_check(f"det {nm} {sq}x{sk} d{d} c{causal} w{window}", x, r, p)
+
+
+def test_bwd_deterministic_varlen(xfa):
+    torch.manual_seed(12)
+    h, hk, d = 4, 2, 128
+    lq, lk = [1, 300, 77, 513, 700], [147, 300, 600, 513, 260]
+    cu_q = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(sum(lq), h, d).bfloat16()
+    k = torch.randn(sum(lk), hk, d).bfloat16()
+    v = torch.randn(sum(lk), hk, d).bfloat16()
+    g = torch.randn(sum(lq), h, d).bfloat16()
+    res = []
+    for _ in range(2):
+        qd, kd, vd = (x.to(DEV).requires_grad_(True) for x in (q, k, v))
+        out = xfa.flash_attn_varlen_func(qd, kd, vd, cu_q.to(DEV), cu_k.to(DEV), max(lq),
+                                         max(lk), causal=True, deterministic=True)
+        res.append([x.cpu() for x in torch.autograd.grad(out, (qd, kd, vd), g.to(DEV))])
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+    dq, dk, dv = res[0]
+    for i in range(len(lq)):
+        qs, gs = q[cu_q[i]:cu_q[i + 1]][None], g[cu_q[i]:cu_q[i + 1]][None]
+        ks, vs = k[cu_k[i]:cu_k[i + 1]][None], v[cu_k[i]:cu_k[i + 1]][None]
+        ref, pt = _oracle_grads(qs, ks, vs, gs, causal=True)
+        got = (dq[cu_q[i]:cu_q[i + 1]][None], dk[cu_k[i]:cu_k[i + 1]][None],
+               dv[cu_k[i]:cu_k[i + 1]][None])
+        for nm, a, r, p in zip(("dq", "dk", "dv"), got, ref, pt):
+            _grad_check(f"det varlen seq{i} {nm}", a, r, p)
 
 
 # Head dims 129..256 (the D = 256 bucket: 4 waves x 32 keys, V rows in registers; the

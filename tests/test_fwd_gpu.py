@@ -2,8 +2,12 @@
 
 Pass rule = the reference's own (test.py:975, 1296, 1593-1594): max|out - out_ref| must be at
 most 2x (fwd, varlen) or 3x + 1e-5 (kvcache) the error of the low-precision PyTorch path
-max|out_pt - out_ref|.  LSE (fp32) is checked against oracle.attention_lse_ref with an absolute
-tolerance of 2e-3 (it accumulates in fp32 from the same fp16/bf16 inputs).
+max|out_pt - out_ref|.  LSE (fp32) is checked against the fp32 log-sum-exp of the oracle
+(oracle.attention_lse_ref) with an absolute tolerance of 2^-9 = 1.95e-3: the kernel's
+normaliser is the sum of the bf16/fp16-ROUNDED P weights that the PV MFMA multiplies (the
+reference sums the fp32 P), and rounding each weight to 8 significant bits moves the sum by at
+most 2^-9 relative, i.e. the LSE by at most 2^-9 absolute.  (The decode kernel sums fp32 P and
+is held to 1e-3.)
 """
 import math
 
@@ -15,7 +19,7 @@ from tests import golden_util as gu
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-LSE_ATOL = 2e-3
+LSE_ATOL = 2.0 ** -9
 
 
 @pytest.fixture(scope="module")
@@ -328,11 +332,9 @@ def test_paged_fp8_generic_staging_bitexact(xfa):
                                        (1, 6, 6, 64), (3, 12, 1, 128)])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("tile16", [0, 1])
-def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype, tile16):
+def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
     """Decode shapes (sq * H/Hk <= 32) through mha_fwd (dense K/V) and through the paged cache,
-    against the oracle; the decode and general kernels agree to rounding.  tile16 = 1 runs the
-    16x16x32 decode tile for groups of <= 16 query rows (option fwd_decode16)."""
+    against the oracle; the decode and general kernels agree to rounding."""
     from xf_flash_attention_cutlass_amd import capi
     L = capi.lib()
     torch.manual_seed(5)
@@ -340,11 +342,7 @@ def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype, tile16):
     q = torch.randn(b, sq, h, d, dtype=dtype)
     k = torch.randn(b, sk, hk, d, dtype=dtype)
     v = torch.randn(b, sk, hk, d, dtype=dtype)
-    assert L.fmha_set_option(b"fwd_decode16", tile16) == 0
-    try:
-        out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
-    finally:
-        L.fmha_set_option(b"fwd_decode16", 0)
+    out = xfa.flash_attn_func(q.to(DEV), k.to(DEV), v.to(DEV), causal=causal)
     r, _ = orc.attention_ref(q, k, v, causal=causal)
     pt, _ = orc.attention_ref(q, k, v, causal=causal, upcast=False, reorder_ops=True)
     _assert_parity(out, r, pt, what="decode dense")

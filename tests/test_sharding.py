@@ -64,6 +64,52 @@ def _worker(rank, world, port, kind, q):
             out, _ = sh.sharded_attention(x, k, v, local_fn=local, causal=True)
             ref = local(x, k, v, causal=True)
             ok = torch.allclose(out, ref, atol=1e-6)
+        elif kind == "heads_alibi":
+            x = torch.randn(2, 24, 8, 16)
+            k = torch.randn(2, 24, 4, 16)
+            v = torch.randn(2, 24, 4, 16)
+            slopes = torch.rand(2, 8)
+
+            def local(qq, kk, vv, causal=False, alibi_slopes=None):
+                bias = orc.alibi_bias(alibi_slopes, qq.shape[1], kk.shape[1], causal=causal)
+                return orc.attention_ref(qq, kk, vv, attn_bias=bias, causal=causal)[0]
+            out, qs = sh.sharded_attention(x, k, v, local_fn=local, causal=True,
+                                           alibi_slopes=slopes)
+            ref = local(x, k, v, causal=True, alibi_slopes=slopes)
+            ok = torch.allclose(out, ref, atol=1e-6) and qs.size == 4
+        elif kind == "batch":
+            # fewer kv heads than ranks: batch shards (uneven: 3 rows over 2 ranks)
+            x = torch.randn(3, 20, 2, 16)
+            k = torch.randn(3, 20, 1, 16)
+            v = torch.randn(3, 20, 1, 16)
+            slopes = torch.rand(3, 2)
+
+            def local(qq, kk, vv, causal=False, alibi_slopes=None):
+                bias = orc.alibi_bias(alibi_slopes, qq.shape[1], kk.shape[1], causal=causal)
+                return orc.attention_ref(qq, kk, vv, attn_bias=bias, causal=causal)[0]
+            out, bs = sh.sharded_attention(x, k, v, local_fn=local, causal=True,
+                                           alibi_slopes=slopes)
+            ref = local(x, k, v, causal=True, alibi_slopes=slopes)
+            ok = torch.allclose(out, ref, atol=1e-6) and bs.size == (2 if rank == 0 else 1)
+        elif kind == "decode":
+            # C5 assembly: batch-sharded paged decode, pages stay in the shared pool
+            b, hk, h, d, page, sk = 5, 2, 8, 16, 4, 37
+            kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.float32)
+            qd = torch.randn(b, 1, h, d)
+            seqlens = torch.tensor([37, 5, 1, 20, 36], dtype=torch.int32)
+
+            def local(qq, kpool, vpool, sl, bt):
+                outs = []
+                for i in range(qq.shape[0]):
+                    n = int(sl[i])
+                    idx = bt[i].long()
+                    kk = kpool[idx].reshape(1, -1, hk, d)[:, :n]
+                    vv = vpool[idx].reshape(1, -1, hk, d)[:, :n]
+                    outs.append(orc.attention_ref(qq[i:i + 1], kk, vv)[0])
+                return torch.cat(outs)
+            out, bs = sh.sharded_decode(qd, kp, vp, seqlens, table, local_fn=local)
+            ref = local(qd, kp, vp, seqlens, table)
+            ok = torch.allclose(out, ref, atol=1e-6) and bs.size == (3 if rank == 0 else 2)
         else:
             lens = [5, 17, 1, 30, 9]
             cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
@@ -87,7 +133,7 @@ def _worker(rank, world, port, kind, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["heads", "varlen"])
+@pytest.mark.parametrize("kind", ["heads", "heads_alibi", "batch", "decode", "varlen"])
 def test_sharded_world2_gloo(kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

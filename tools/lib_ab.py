@@ -46,7 +46,7 @@ def main():
             tmp = os.path.join(tempfile.mkdtemp(), f"v{i}_" + os.path.basename(path))
             shutil.copy(path, tmp)
             path = tmp
-        lib = capi.load(path)
+        lib = capi.load(path, strict=False)
         for o in a.opt + ([x for x in opts.split(",") if x] if opts else []):
             name, val = o.split("=")
             assert lib.fmha_set_option(name.encode(), int(val)) == 0, lib.fmha_last_error()

@@ -29,30 +29,37 @@ _SIGS = {
                                  vp],
     "fmha_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                  f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz],
-    "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32],
+    "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
     "fmha_varlen_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
-                        i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp, vp, sz],
-    "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32],
+                        i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz, vp],
+    "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
     "fmha_kvcache_append": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, b_,
                             b_, i32, i32, i32, i32, i32, b_, vp],
     "fmha_last_error": [],
     "fmha_last_status": [],
+    "fmha_last_num_splits": [],
     "fmha_version": [],
     "fmha_set_option": [C.c_char_p, C.c_int],
+    "fmha_get_option": [C.c_char_p],
 }
 _RES = {"fmha_last_error": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
-        "fmha_set_option": C.c_int,
+        "fmha_last_num_splits": C.c_int,
+        "fmha_set_option": C.c_int, "fmha_get_option": C.c_int,
         "fmha_bwd_workspace_size": sz, "fmha_varlen_bwd_workspace_size": sz}
 
 EXPORTED = tuple(_SIGS)
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
+def load(path: str = LIB_PATH, strict: bool = True) -> C.CDLL:
+    """Load a build of the library; strict=False tolerates symbols an older build (an A/B
+    variant, tools/lib_ab.py) does not export."""
     if not os.path.exists(path):
         raise ImportError(f"native library {path} is missing: run `python "
                           "xf_flash_attention_cutlass_amd/build.py` (no CPU fallback exists)")
     lib = C.CDLL(path)
     for name, args in _SIGS.items():
+        if not strict and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RES.get(name, None)

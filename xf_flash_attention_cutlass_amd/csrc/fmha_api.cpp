@@ -37,6 +37,7 @@ namespace {
 
 thread_local std::string g_err;
 thread_local int g_status = 0;
+thread_local int g_last_splits = 0;     // split count of this thread's last forward launch
 
 void clear_error() { g_err.clear(); g_status = 0; }
 bool fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -92,15 +93,35 @@ int* counter_get(hipStream_t st) {
     return c;
 }
 
-int g_num_cus = 0;
-int num_cus() {
-    if (g_num_cus == 0) {
-        int dev = 0, n = 0;
-        hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        g_num_cus = n;
-    }
-    return g_num_cus;
+// CU count per device (a process may drive several GPUs; cached per device id)
+int num_cus(int dev) {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+    return n;
+}
+int current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return dev;
+}
+
+// Kernels address one sequence's rows of one tensor with 32-bit byte offsets from a buffer
+// descriptor (and mark skipped lanes with kOOB = 0x7FFFFF00), so one sequence's slab of any
+// tensor must stay below that (the reference's 64-bit index_t has no such limit; a slab this
+// large is >= 256k tokens x 32 heads x d128 in bf16).
+constexpr int64_t kMaxSlabBytes = 0x7FFFFF00LL;
+bool slab_ok(const char* what, int64_t rows, int64_t row_elems, int esz) {
+    const int64_t bytes = rows * row_elems * esz;
+    if (bytes < kMaxSlabBytes) return true;
+    return fail(1, "%s: one sequence spans %lld bytes (%lld rows x %lld elements); this build "
+                "addresses a sequence with 32-bit offsets and supports < %lld bytes",
+                what, (long long)bytes, (long long)rows, (long long)row_elems, (long long)kMaxSlabBytes);
 }
 
 // Reference heuristic (paged_attn.cpp:128-163): the smallest split count whose wave
@@ -180,29 +201,40 @@ void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
 
 // Split scratch + launch (shared by every forward entry).
 void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
+    Options& o = options();
+    p.device = current_device();
+    p.num_cus = num_cus(p.device);
+    p.waves = o.fwd_waves.load();
+    p.persist_per_cu = o.fwd_persistent.load();
+    p.order = o.fwd_order.load();
+    p.xcdq = o.fwd_xcdq.load();
+    p.prio_hi = o.fwd_prio.load();
+    p.pipe = o.fwd_pipe.load();
+    p.max_slack = (float)o.fwd_slack.load();
     const int n_blocks = (p.seqlen_k + kBlockN - 1) / kBlockN;
     int splits = num_splits_req;
     // Decode: the whole GQA group of query rows fits one 32-row MFMA tile -> the split-KV
     // decode kernel (every wave a split, fmha_decode_kernel.h); splits a multiple of 4.
-    p.decode = options().fwd_decode && !p.cu_seqlens_q && !p.cu_seqlens_k &&
+    p.decode = o.fwd_decode.load() && !p.cu_seqlens_q && !p.cu_seqlens_k &&
                p.seqlen_q * p.group <= 32 && hd_bucket(p.d) == p.d && p.d <= 128 &&
                (!p.block_table || p.page_size % 16 == 0);
     if (p.decode) {
         const int tiles = (p.seqlen_k + 31) / 32;
         const int work = p.b * p.hk;
         int zs = num_splits_req > 0 ? (num_splits_req + 3) / 4
-                                    : (options().dec_wg_per_cu * num_cus() + work - 1) / work;
+                                    : (o.dec_wg_per_cu.load() * p.num_cus + work - 1) / work;
         zs = std::max(1, std::min(zs, std::max(1, tiles / 8)));
         zs = std::min(zs, 32);
         splits = 4 * zs;
     } else if (p.cu_seqlens_q) {
         splits = 1;  // varlen: single pass (the reference forces it too)
     } else if (splits <= 0) {
-        const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group, p.d);
-        splits = num_splits_heuristic(work, num_cus() * 2, n_blocks, 128);
+        const int work = p.b * p.hk * fwd_num_m_blocks(p.seqlen_q, p.group, p.d, p.waves);
+        splits = num_splits_heuristic(work, p.num_cus * 2, n_blocks, 128);
     }
     if (!p.decode) splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
     p.num_splits = splits;
+    g_last_splits = splits;
     if (splits > 1) {
         const int hd = hd_bucket(p.d);
         const size_t rows = (size_t)p.b * p.h * p.seqlen_q;
@@ -212,17 +244,13 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         p.oaccum = (float*)base;
         p.lseaccum = (float*)(base + (size_t)splits * rows * hd * sizeof(float));
     }
-    p.prio_hi = options().fwd_prio;
-    p.sched_mode = options().fwd_sched;
-    p.store8 = options().fwd_store8;
-    p.pipe = options().fwd_pipe;
-    p.dbg = options().fwd_dbg;
-    p.max_slack = (float)options().fwd_slack;
     // dynamic item queue: ragged (varlen) row blocks balance across CUs as they finish
     p.work_ctr = nullptr;
-    const int dyn = options().fwd_dyn;
-    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && p.cu_seqlens_q))) p.work_ctr = counter_get(st);
-    options().num_cus = num_cus();
+    const int dyn = o.fwd_dyn.load();
+    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && p.cu_seqlens_q))) {
+        p.work_ctr = counter_get(st);
+        if (!p.work_ctr) { fail(3, "could not allocate the item-queue counters"); return; }
+    }
     hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
 }
 
@@ -232,39 +260,43 @@ extern "C" {
 
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
+int fmha_last_num_splits(void) { return g_last_splits; }
 const char* fmha_version(void) { return "xf-fmha-gfx950 1.0"; }
 
 int fmha_set_option(const char* name, int value) {
     clear_error();
     if (!name) { fail(1, "option name is null"); return -1; }
-    if (!strcmp(name, "fwd_waves")) {
-        if (value != 4 && value != 8) { fail(1, "fwd_waves must be 4 or 8"); return -1; }
-        options().fwd_waves = value;
+    Options& o = options();
+    struct Knob { const char* name; std::atomic<int>* slot; int lo, hi; };
+    const Knob knobs[] = {
+        {"fwd_waves", &o.fwd_waves, 4, 8},       {"fwd_prio", &o.fwd_prio, 0, 1},
+        {"fwd_persistent", &o.fwd_persistent, 0, 8}, {"fwd_slack", &o.fwd_slack, 0, 16},
+        {"fwd_order", &o.fwd_order, 0, 1},       {"fwd_dyn", &o.fwd_dyn, 0, 2},
+        {"fwd_xcdq", &o.fwd_xcdq, 0, 1},         {"fwd_pipe", &o.fwd_pipe, 0, 2},
+        {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
+    };
+    for (const Knob& k : knobs) {
+        if (strcmp(name, k.name)) continue;
+        if (value < k.lo || value > k.hi || (k.slot == &o.fwd_waves && value != 4 && value != 8)) {
+            fail(1, "option %s: value %d out of range [%d, %d]", name, value, k.lo, k.hi);
+            return -1;
+        }
+        k.slot->store(value);
         return 0;
     }
-    if (!strcmp(name, "fwd_prio")) { options().fwd_prio = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_pp")) { options().fwd_pp = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_sched")) { options().fwd_sched = value; return 0; }
-    if (!strcmp(name, "fwd_store8")) { options().fwd_store8 = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_persistent")) { options().fwd_persistent = value < 0 ? 0 : value; return 0; }
-    if (!strcmp(name, "fwd_pipe")) { options().fwd_pipe = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
-    if (!strcmp(name, "fwd_slack")) {
-        if (value < 0 || value > 16) { fail(1, "fwd_slack must be in [0, 16]"); return -1; }
-        options().fwd_slack = value;
-        return 0;
-    }
-    if (!strcmp(name, "fwd_order")) { options().fwd_order = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_dyn")) { options().fwd_dyn = value < 0 ? 0 : (value > 2 ? 2 : value); return 0; }
-    if (!strcmp(name, "fwd_xcdq")) { options().fwd_xcdq = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "bwd_prio")) { options().bwd_prio = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "dec_wg_per_cu")) {
-        if (value < 1 || value > 16) { fail(1, "dec_wg_per_cu must be in [1, 16]"); return -1; }
-        options().dec_wg_per_cu = value;
-        return 0;
-    }
-    if (!strcmp(name, "fwd_dbg")) { options().fwd_dbg = value; return 0; }
-    if (!strcmp(name, "fwd_decode")) { options().fwd_decode = value ? 1 : 0; return 0; }
-    if (!strcmp(name, "fwd_decode16")) { options().fwd_decode16 = value ? 1 : 0; return 0; }
+    fail(1, "unknown option '%s'", name);
+    return -1;
+}
+
+int fmha_get_option(const char* name) {
+    clear_error();
+    Options& o = options();
+    if (!name) { fail(1, "option name is null"); return -1; }
+#define XFA_GET(n) if (!strcmp(name, #n)) return o.n.load();
+    XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
+    XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
+    XFA_GET(dec_wg_per_cu)
+#undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;
 }
@@ -282,6 +314,8 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
         REQUIRE(p_dropout == 0.f, "dropout is not supported by the forward C path (p_dropout=%g)", p_dropout);
         REQUIRE(!return_softmax, "return_softmax is only supported with dropout, which this build does not support");
+        if (!slab_ok("q/o", seqlen_q, (int64_t)num_heads * head_size, 2) ||
+            !slab_ok("k/v", seqlen_k, (int64_t)num_heads_k * head_size, 2)) return;
         FwdParams p{};
         p.q = q_ptr; p.k = k_ptr; p.v = v_ptr; p.o = o_ptr;
         p.lse = (float*)softmax_lse_ptr;
@@ -314,6 +348,8 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                 "cu_seqlens_q and cu_seqlens_k (or a block table) must be given");
         REQUIRE(max_seqlen_q > 0 && max_seqlen_k >= 0, "max_seqlen_q must be positive");
         if (max_seqlen_k == 0) { fail(1, "max_seqlen_k == 0: nothing to attend to"); return; }
+        if (!slab_ok("q/o", max_seqlen_q, (int64_t)num_heads * head_size, 2) ||
+            (!block_table && !slab_ok("k/v", max_seqlen_k, (int64_t)num_heads_k * head_size, 2))) return;
         FwdParams p{};
         p.q = q; p.k = k; p.v = v; p.o = o; p.lse = (float*)softmax_lse;
         const int h = num_heads, hk = num_heads_k, d = head_size;
@@ -381,6 +417,9 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
         REQUIRE(page_block_size > 0, "page_block_size must be positive");
         REQUIRE(seqlen_q > 0 && max_seqlen_k > 0, "seqlen_q / seqlen_k must be positive");
         REQUIRE(kv_dtype == 0 || kv_dtype == 1, "kv_dtype must be 0 (same as q) or 1 (fp8 e4m3fn)");
+        REQUIRE(block_table_stride > 0, "block_table_stride must be positive");
+        if (!slab_ok("q/o", seqlen_q, (int64_t)num_heads * head_size, 2) ||
+            !slab_ok("kcache/vcache page", page_block_size, (int64_t)num_heads_k * head_size, kv_dtype == 1 ? 1 : 2)) return;
         FwdParams p{};
         const int h = num_heads, hk = num_heads_k, d = head_size;
         p.q = q; p.k = kcache; p.v = vcache; p.o = o; p.lse = (float*)softmax_lse;
@@ -423,6 +462,9 @@ void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const
         REQUIRE(head_size > 0 && head_size % 8 == 0 && head_size <= 256,
                 "head_size must be a multiple of 8 (<= 256) for the append pass");
         REQUIRE(page_block_size > 0, "page_block_size must be positive");
+        REQUIRE(block_table_stride > 0, "block_table_stride must be positive");
+        // the kernel reads cache_seqlens while writing seqlens_out: in-place is a race
+        REQUIRE(seqlens_out != cache_seqlens, "seqlens_out must not alias cache_seqlens");
         REQUIRE(rotary_dim >= 0 && rotary_dim <= head_size && rotary_dim % 16 == 0,
                 "Only rotary dimensions divisible by 16 and <= headdim are supported");
         REQUIRE(rotary_dim == 0 || (rotary_cos && rotary_sin && q && q_out),
@@ -471,21 +513,39 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
 
 
 // ------------------------------------------------------------------ backward -----------
-static size_t bwd_ws_bytes(int64_t tokens, int h, int d) {
-    const int hd = hd_bucket(d);
-    const size_t acc = (size_t)tokens * h * hd * sizeof(float);
+// Workspace: fp32 dq_accum [tokens][h][HD] (deterministic: one such slice per key block of the
+// longest sequence) + fp32 D = rowsum(dO*O) [tokens][h].
+static int bwd_block_n_host(int d) { return hd_bucket(d) > 128 ? 128 : 256; }
+static int bwd_slices(int max_seqlen_k, int d, bool det) {
+    return det ? (max_seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d) : 1;
+}
+static size_t bwd_acc_bytes(int64_t tokens, int h, int d) {
+    return (((size_t)tokens * h * hd_bucket(d) * sizeof(float)) + 255) / 256 * 256;
+}
+static size_t bwd_ws_bytes(int64_t tokens, int h, int d, int slices) {
     const size_t dsum = (size_t)tokens * h * sizeof(float);
-    return ((acc + 255) / 256) * 256 + ((dsum + 255) / 256) * 256;
+    return (size_t)slices * bwd_acc_bytes(tokens, h, d) + ((dsum + 255) / 256) * 256;
 }
 
-size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t /*seqlen_k*/, int32_t batch_size,
-                               int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size) {
-    return bwd_ws_bytes((int64_t)batch_size * seqlen_q, num_heads, head_size);
+size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
+                               int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size,
+                               bool deterministic) {
+    return bwd_ws_bytes((int64_t)batch_size * seqlen_q, num_heads, head_size,
+                        bwd_slices(seqlen_k, head_size, deterministic));
 }
 
-size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t /*total_k*/, int32_t /*batch_size*/,
-                                      int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size) {
-    return bwd_ws_bytes(total_q, num_heads, head_size);
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t /*batch_size*/,
+                                      int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size,
+                                      bool deterministic) {
+    return bwd_ws_bytes(total_q, num_heads, head_size,
+                        bwd_slices(max_seqlen_k, head_size, deterministic));
+}
+
+// The pre / convert kernels index (token, head, 16-byte chunk) with one 32-bit thread id.
+static bool bwd_rows_ok(int64_t tokens, int h, int d) {
+    const int64_t threads = tokens * h * (hd_bucket(d) / 8);
+    if (threads < (1LL << 31) - 256) return true;
+    return fail(1, "backward: %lld (token, head) rows exceed the 32-bit thread index", (long long)(tokens * h));
 }
 
 static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl, int wr,
@@ -498,7 +558,7 @@ static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl,
     p.scale = softmax_scale;
     p.scale_log2 = scale_softmax * 1.4426950408889634f;
     p.alibi_mul = 1.f / scale_softmax;
-    p.prio_hi = options().bwd_prio;
+    p.device = current_device();
     return true;
 }
 
@@ -506,7 +566,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
               void* dk, void* dv, void* alibi_slopes, void* softmax_d, int32_t seqlen_q,
               int32_t seqlen_k, int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
               int32_t head_size, float p_dropout, float softmax_scale, int window_size_left,
-              int window_size_right, float softcap, bool /*deterministic*/, bool is_fp16,
+              int window_size_right, float softcap, bool deterministic, bool is_fp16,
               hipStream_t stream, void* workspace, size_t workspace_bytes) {
     try {
         clear_error();
@@ -516,7 +576,12 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
         REQUIRE(p_dropout == 0.f, "dropout is not supported by the backward (p_dropout=%g)", p_dropout);
         const int h = num_heads, hk = num_heads_k, d = head_size;
-        const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d);
+        if (!slab_ok("q/out/dout/dq", seqlen_q, (int64_t)h * d, 2) ||
+            !slab_ok("k/v/dk/dv", seqlen_k, (int64_t)hk * d, 2) ||
+            !slab_ok("dq_accum", seqlen_q, hd_bucket(d), 4) ||
+            !bwd_rows_ok((int64_t)batch_size * seqlen_q, h, d)) return;
+        const int slices = bwd_slices(seqlen_k, d, deterministic);
+        const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d, slices);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
@@ -526,8 +591,10 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout; p.lse = (const float*)softmax_lse;
         p.dq = dq; p.dk = dk; p.dv = dv;
         p.dq_accum = (float*)ws;
-        const size_t acc = (size_t)batch_size * seqlen_q * h * hd * sizeof(float);
-        p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + ((acc + 255) / 256) * 256);
+        const size_t acc = bwd_acc_bytes((int64_t)batch_size * seqlen_q, h, d);
+        p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
+        p.dq_slices = deterministic ? slices : 0;
+        p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = (int64_t)seqlen_q * h * d;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = p.q_batch;
         p.do_row = p.q_row; p.do_head = d; p.do_batch = p.q_batch;
@@ -555,8 +622,9 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
                      int32_t max_seqlen_k, int32_t total_q, int32_t total_k,
                      int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
                      int32_t head_size, float softmax_scale, int window_size_left,
-                     int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
-                     void* workspace, size_t workspace_bytes) {
+                     int window_size_right, float softcap, bool deterministic, bool is_fp16,
+                     hipStream_t stream, void* workspace, size_t workspace_bytes,
+                     void* softmax_d) {
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
@@ -566,7 +634,11 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         REQUIRE(total_q > 0 && total_k > 0 && max_seqlen_q > 0 && max_seqlen_k > 0,
                 "total/max sequence lengths must be positive");
         const int h = num_heads, hk = num_heads_k, d = head_size;
-        const size_t need = bwd_ws_bytes(total_q, h, d);
+        if (!slab_ok("q/out/dout/dq", max_seqlen_q, (int64_t)h * d, 2) ||
+            !slab_ok("k/v/dk/dv", max_seqlen_k, (int64_t)hk * d, 2) ||
+            !bwd_rows_ok(total_q, h, d)) return;
+        const int slices = bwd_slices(max_seqlen_k, d, deterministic);
+        const size_t need = bwd_ws_bytes(total_q, h, d, slices);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
@@ -576,8 +648,10 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.q = q; p.k = k; p.v = v; p.o = out; p.dout = dout; p.lse = (const float*)softmax_lse;
         p.dq = dq; p.dk = dk; p.dv = dv;
         p.dq_accum = (float*)ws;
-        const size_t acc = (size_t)total_q * h * hd * sizeof(float);
-        p.dsum = (float*)(ws + ((acc + 255) / 256) * 256);
+        const size_t acc = bwd_acc_bytes(total_q, h, d);
+        p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
+        p.dq_slices = deterministic ? slices : 0;
+        p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = 0;
         p.do_row = p.q_row; p.do_head = d; p.do_batch = 0;

@@ -98,6 +98,9 @@ __global__ void __launch_bounds__(256) fmha_append_kernel(const AppendParams p) 
         const int j = (int)(bj % p.snew);
         const int bi = (int)(bj / p.snew);
         const int pos = p.cache_seqlens[bi] + j;
+        // a slot past the block table's row (cache full) is dropped, never written into
+        // another sequence's page
+        if (pos < 0 || pos / p.page >= p.bt_stride) return;
         const int pg = p.block_table[(int64_t)bi * p.bt_stride + pos / p.page];
         const int64_t slot = (int64_t)pg * p.page_stride + (int64_t)(pos % p.page) * p.row_stride +
                              (int64_t)hki * p.head_stride;

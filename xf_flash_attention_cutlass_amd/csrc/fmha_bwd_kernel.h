@@ -6,17 +6,19 @@
 // `convert_dQ` (flash_bwd_preprocess_kernel_hip.h:184-270) and host-side GQA reduction
 // (export.cpp:1165-1168).  Same math here, re-designed for CDNA4:
 //
-//  * one workgroup = 4 waves (one per SIMD, the whole 512-entry register file each) = 256 keys
-//    of one (batch, kv-head); each wave owns 64 keys and keeps dK^T and dV^T of them in
-//    (accumulation) registers while the workgroup sweeps every query head of the GQA group x
-//    32-row query tiles — dK/dV need no cross-workgroup (or host) reduction;
+//  * one workgroup = 256 keys (D <= 128; 128 keys for D > 128) of one (batch, kv-head); each
+//    wave owns 32 (D = 64: 64) keys and keeps dK^T and dV^T of them in accumulation registers
+//    while the workgroup sweeps every query head of the GQA group x 32-row query tiles —
+//    dK/dV need no cross-workgroup (or host) reduction;
 //  * key-on-the-lane orientation: S = Q K^T and dP = dO V^T land with the key on the MFMA
 //    lane, so (after a pairwise cvt) P and dS are directly the B operands of
 //    dV^T += dO^T P and dK^T += Q^T dS (v_mfma_f32_32x32x16); dO^T / Q^T come from the same
 //    swizzled LDS tile through ds_read_b64_tr_b16;
 //  * dS crosses LDS once (as dS^T, bf16) for dQ = dS K, computed with v_mfma_f32_16x16x32 by
 //    all waves and added to an fp32 dQ accumulator with global float atomics (256 keys per
-//    workgroup => 640 MFMA flops per atomic byte, cdna_hip_programming.md Appendix B);
+//    workgroup => 640 MFMA flops per atomic byte, cdna_hip_programming.md Appendix B), or, in
+//    deterministic mode (export.cpp:1086-1092 splits dq_accum the same way), stored into the
+//    key block's own accumulator slice and summed in key-block order by the convert kernel;
 //  * P is recomputed from the forward LSE; D = rowsum(dO*O) comes from the preprocess kernel.
 #pragma once
 
@@ -24,14 +26,11 @@
 
 namespace xfa {
 
-#ifndef XFA_BWD_WAVES
-#define XFA_BWD_WAVES 8
-#endif
 // Waves per workgroup.  D = 128: 8 waves x 32 keys, two waves per SIMD (256 registers each)
-// so one wave's LDS / global waits hide behind the other's MFMAs.  D = 64 (or
-// XFA_BWD_WAVES=4): 4 waves x 64 keys, one wave per SIMD with 512 registers (a 32-row D=64
-// Q tile has too few 16-byte chunks for 512 threads).
-template <int HD> constexpr int bwd_waves() { return HD == 128 ? XFA_BWD_WAVES : 4; }
+// so one wave's LDS / global waits hide behind the other's MFMAs.  D = 64: 4 waves x 64 keys,
+// one wave per SIMD with 512 registers (a 32-row D=64 Q tile has too few 16-byte chunks for
+// 512 threads).
+template <int HD> constexpr int bwd_waves() { return HD == 128 ? 8 : 4; }
 // Keys per workgroup: 256, or 128 for D = 129..256 (4 waves x 32 keys: the 32 x 256 dK^T and
 // dV^T accumulators take 256 of a wave's 512 registers).
 template <int HD> constexpr int bwd_block_n() { return HD > 128 ? 128 : 256; }
@@ -42,24 +41,12 @@ template <int HD> constexpr size_t bwd_smem_bytes() {
     return (bwd_v_in_regs<HD>() ? 1 : 2) * (size_t)bwd_block_n<HD>() * HD * 2 + 2 * (size_t)32 * HD * 2 +
            (size_t)bwd_block_n<HD>() * 64;
 }
-#ifndef XFA_BWD_DQ32
-#define XFA_BWD_DQ32 0
-#endif
-#ifndef XFA_BWD_EARLYSTORE
-#define XFA_BWD_EARLYSTORE 1
-#endif
-#ifndef XFA_BWD_NOATOMIC
-#define XFA_BWD_NOATOMIC 0
-#endif
-// dQ partial sums -> the fp32 accumulator (XFA_BWD_NOATOMIC: timing experiment only, the
-// values are consumed but never added)
-__device__ __forceinline__ void dq_atomic_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
-#if XFA_BWD_NOATOMIC
-    asm volatile("" ::"v"(v));
-    (void)r; (void)off;
-#else
-    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
-#endif
+// dQ partial sums -> the fp32 accumulator: float atomics into one [rows][HD] accumulator, or
+// (deterministic) plain stores into this key block's own slice, summed in key-block order by
+// the convert kernel
+__device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off, bool det) {
+    if (det) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
 }
 constexpr int kBwdBlockM = 32;               // query rows per tile
 
@@ -114,13 +101,16 @@ __global__ void __launch_bounds__(256) fmha_bwd_pre_kernel(const BwdParams p, in
     for (int m = TPR / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
     const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + pos;
     if (c == 0) p.dsum[li] = acc;
+    if (p.dq_slices) return;    // deterministic: every slice row read by convert is stored first
     float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
                 (int64_t)pos * p.acc_row + d0;
     *reinterpret_cast<f32x4_t*>(qa) = f32x4_t{0.f, 0.f, 0.f, 0.f};
     *reinterpret_cast<f32x4_t*>(qa + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
 }
 
-// dQ = dQaccum * scale -> dtype
+// dQ = dQaccum * scale -> dtype.  Deterministic mode: dQaccum = the sum, in key-block order, of
+// the slices of the key blocks whose query-tile sweep covered this row (the same [p_lo, p_hi)
+// tile range the main kernel computes; other slice rows are never written).
 template <int HD, typename T>
 __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p, int total_rows) {
     constexpr int TPR = HD / 8;
@@ -137,10 +127,45 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
     if (d0 >= p.d) return;
     const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
                       (int64_t)pos * p.acc_row + d0;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    if (!p.dq_slices) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = qa[j];
+    } else {
+        constexpr int BN = bwd_block_n<HD>();
+        int sq = p.seqlen_q, sk = p.seqlen_k, lpos = pos;
+        if (p.cu_seqlens_q) {     // varlen: the sequence holding global token `tok`
+            int lo = 0, hi = p.b - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (p.cu_seqlens_q[mid] <= tok) lo = mid; else hi = mid - 1;
+            }
+            lpos = tok - p.cu_seqlens_q[lo];
+            sq = p.cu_seqlens_q[lo + 1] - p.cu_seqlens_q[lo];
+            sk = p.cu_seqlens_k[lo + 1] - p.cu_seqlens_k[lo];
+        }
+        const bool mask = p.wl >= 0 || p.wr >= 0;
+        const int diag = sk - sq;
+        const int tile = lpos / kBwdBlockM;
+        for (int j = 0; j < p.dq_slices; ++j) {
+            const int n0 = j * BN;
+            if (n0 >= sk) break;
+            int p_lo = 0, p_hi = sq;
+            if (mask && p.wr >= 0) p_lo = max(0, n0 - diag - p.wr);
+            if (mask && p.wl >= 0) p_hi = min(sq, n0 + BN - 1 - diag + p.wl + 1);
+            if (p_hi <= p_lo) continue;
+            if (tile < p_lo / kBwdBlockM || tile >= (p_hi + kBwdBlockM - 1) / kBwdBlockM) continue;
+            const float* sl = qa + (int64_t)j * p.acc_slice;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += sl[u];
+        }
+    }
     typedef __attribute__((ext_vector_type(8))) T T8;
     T8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (T)(qa[j] * p.scale);
+    for (int j = 0; j < 8; ++j) v[j] = (T)(acc[j] * p.scale);
     T* dq = reinterpret_cast<T*>(p.dq) + (int64_t)bidx * p.dq_batch + (int64_t)pos * p.dq_row +
             (int64_t)head * p.dq_head + d0;
     *reinterpret_cast<T8*>(dq) = v;
@@ -336,14 +361,6 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         }
     }
 
-#if XFA_BWD_DQ32
-    // dS^T tr-read bases for the 32x32x16 dQ product (rows of a 16-key slice, q column quad)
-    int dq32_aoff[2];
-#pragma unroll
-    for (int part = 0; part < 2; ++part)
-        dq32_aoff[part] = ds_off(4 * hh + q4 + 8 * part, 16 * ((lane >> 4) & 1) + 4 * (lane & 3));
-#endif
-
     // (D > 128: the dQ K-read offsets are recomputed per use instead of held in registers)
     auto dqb = [&](const int i, const int part) {
         if constexpr (HD > 128) {
@@ -362,7 +379,8 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
-    if (p.prio_hi && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    const bool det = p.dq_slices > 0;
+    float* const dq_base = p.dq_accum + (det ? (int64_t)blockIdx.y * p.acc_slice : 0);
     float lsd_cur = 0.f;
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible
@@ -480,44 +498,10 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             }
         }
         __syncthreads();
-#if XFA_BWD_EARLYSTORE
         // Q / dO of this tile are dead after the barrier above (dQ reads only dS^T and K)
         if (it + 1 < n_iter) store_q();
         lsd_cur = lsd_value();      // every vmcnt wait of the iteration comes before its atomics
         asm volatile("" : "+v"(lsd_cur));   // (pinned: not sunk below the atomics)
-#endif
-#if XFA_BWD_DQ32
-        // ---- dQ[q][32 dt .. +32) += dS K over the 256 keys on v_mfma_f32_32x32x16 by waves
-        // 0..ND-1 (one per SIMD).  A = dS (q on the lane) and B = K (d on the lane) are both
-        // transposing reads of key-row images with the same lane -> (row, column) pattern, so
-        // both carry the same key order.  One accumulator register = two 128-byte row segments
-        // of dQ (rows m, m + 4), the full-rate float-atomic shape (MI355X_MICROARCH.md).
-        static_assert(ND <= NW, "XFA_BWD_DQ32: one 32-column dQ tile per wave");
-        if (wave < ND) {
-            const int dt = wave;
-            f32x16 dq = f32x16{};
-#pragma unroll
-            for (int ks = 0; ks < BN / 16; ++ks) {
-                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 16 * 64 + dq32_aoff[0]));
-                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 16 * 64 + dq32_aoff[1]));
-                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(k_lds + ks * 16 * HD * 2 + troff(0, dt)));
-                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(k_lds + ks * 16 * HD * 2 + troff(1, dt)));
-                const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-                dq = DT<T>::mfma32(__builtin_bit_cast(V8, av), __builtin_bit_cast(V8, bv), dq);
-            }
-            const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
-                              (int64_t)(q_off + q0) * p.acc_row;
-            const __amdgpu_buffer_rsrc_t qrs =
-                make_rsrc(qa, (uint32_t)(max(0, sq - q0) * p.acc_row * 4));
-            const int arow = (int)p.acc_row * 4;
-            const int d = 32 * dt + lr;
-            const int base = d < p.d ? (4 * hh) * arow + d * 4 : kOOB;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                dq_atomic_add(dq[r], qrs, base + (8 * (r >> 2) + (r & 3)) * arow);
-        }
-#else
         // ---- dQ[q][d] += dS K over the 256 keys (16x16x32; A = dS via tr-read of dS^T)
         {
             f32x4 dq[NDQ];
@@ -542,7 +526,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             }
             // buffer atomics over this (batch, head)'s rows [q0, sq): rows past the end and the
             // padded head-dim columns fall outside the descriptor and are dropped (no branches)
-            const float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+            const float* qa = dq_base + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
                               (int64_t)(q_off + q0) * p.acc_row;
             const __amdgpu_buffer_rsrc_t qrs =
                 make_rsrc(qa, (uint32_t)(max(0, sq - q0) * p.acc_row * 4));
@@ -553,14 +537,9 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 const int base = d < p.d ? (16 * mt + 4 * g16) * arow + d * 4 : kOOB;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    dq_atomic_add(dq[i][r], qrs, base + r * arow);
+                    dq_add(dq[i][r], qrs, base + r * arow, det);
             }
         }
-#endif
-#if !XFA_BWD_EARLYSTORE
-        if (it + 1 < n_iter) store_q();
-        lsd_cur = lsd_value();
-#endif
         __syncthreads();
     }
 

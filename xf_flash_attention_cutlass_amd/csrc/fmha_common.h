@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <type_traits>
 
 namespace xfa {
@@ -19,6 +20,14 @@ __device__ __forceinline__ void static_for(F&& f) {
         f(std::integral_constant<int, I>{});
         static_for<N, I + 1>(f);
     }
+}
+
+// Per-device one-time host action (kernel attributes are set per device: a process may drive
+// several GPUs).  Returns true exactly once per (flag word, device) for devices 0..63.
+inline bool first_on_device(std::atomic<unsigned long long>& done, int device) {
+    if (device < 0 || device >= 64) return true;
+    const unsigned long long bit = 1ull << device;
+    return !(done.fetch_or(bit) & bit);
 }
 
 // ------------------------------------------------------------------ vector types --
@@ -89,17 +98,21 @@ struct FwdParams {
     int kv_fp8;                // 1: K/V stored as fp8 e4m3fn
     float k_scale, v_scale;
     int prio_hi;               // 1: waves NW/2.. run at s_setprio 1 (static, guide T5)
-    int sched_mode;            // bit0/bit1: pinned read-ahead interleave in PV / QK^T (pp)
-    int store8;                // 1: legacy 8-byte O stores (A/B knob for the 16-byte tail)
     int persistent;            // 1: persistent grid walking (row block, b*hk) items
     int n_mblocks;             // row blocks per (b, kv head) (persistent mode)
     int pipe;                  // 1: software-pipelined loop over the unmasked key tiles
-    int dbg;                   // timing experiments only (results invalid when set)
     float max_slack;           // log2 units the running max may lag the true max before the
                                // O / l rescale (deferred rescale; 0 = rescale on every rise)
     int decode;                // 1: run fmha_decode_kernel (split-KV decode)
     int* work_ctr;             // persistent == 3: self-resetting counters [-, finished, next x 8]
     int xcd_queues;            // persistent == 3: one item queue per XCD (else queue 0 only)
+    // host-side launch choices (snapshotted from the options by the C ABI, per call)
+    int waves;                 // 4 or 8 waves per workgroup (D <= 128)
+    int num_cus;               // CUs of the current device
+    int persist_per_cu;        // persistent workgroups per CU (0 = one workgroup per item)
+    int order;                 // persistent item order (0 boustrophedon, 1 XCD-grouped pairs)
+    int xcdq;                  // dynamic queue kind (1 per-XCD queues)
+    int device;                // current device id (per-device one-time kernel attributes)
 };
 
 struct CombineParams {
@@ -118,8 +131,6 @@ struct BwdParams {
     void* dq; void* dk; void* dv;
     float* dq_accum;     // fp32 [b][h][seqlen_q_pad][HD] (varlen: [h][total_q_pad][HD])
     float* dsum;         // fp32 rowsum(dO*O), layout like lse
-    float* dk_accum;     // fp32 GQA partial accumulators or null
-    float* dv_accum;
 
     int64_t q_batch, q_row, q_head;
     int64_t k_batch, k_row, k_head;
@@ -145,7 +156,9 @@ struct BwdParams {
     float softcap_pre;
     float alibi_mul;
     int softcap_on;
-    int prio_hi;         // 1: waves NW/2.. run at s_setprio 1 (A/B knob)
+    int dq_slices;       // deterministic: dQ partials per key block in dq_accum slices (0 = atomics)
+    int64_t acc_slice;   // floats between dq_accum slices
+    int device;          // current device id (per-device one-time kernel attributes)
 };
 
 // ------------------------------------------------------------------ dtype traits --
@@ -239,20 +252,6 @@ __device__ __forceinline__ void store_o_row16(T* orow, const f32x16 (&acc)[ND], 
             const int col = 32 * dt + 8 * gp + 8 * hh;
             if (col < d) *reinterpret_cast<u32x4*>(orow + col) = u32x4{r0[0], r1[0], r0[1], r1[1]};
         }
-}
-
-template <typename T, int ND>
-__device__ __forceinline__ void store_o_row8(T* orow, const f32x16 (&acc)[ND], float inv, int d, int hh) {
-    typedef __attribute__((ext_vector_type(4))) T T4;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-            if (32 * dt + 8 * g < d) {
-                const T4 v = {(T)(acc[dt][4 * g] * inv), (T)(acc[dt][4 * g + 1] * inv),
-                              (T)(acc[dt][4 * g + 2] * inv), (T)(acc[dt][4 * g + 3] * inv)};
-                *reinterpret_cast<T4*>(orow + 32 * dt + 8 * g + 4 * hh) = v;
-            }
 }
 
 // 8 OCP fp8 e4m3fn values (two dwords) -> 8 x T = T(f32(fp8) * scale), packed in 4 dwords.

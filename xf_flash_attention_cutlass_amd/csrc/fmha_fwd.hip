@@ -1,9 +1,8 @@
 // fmha_fwd.hip — forward instantiations for one (head dim, dtype) pair.
-// Compiled once per pair with -DXFA_HD=<64|128> -DXFA_DT=<bf16|f16> (see build.py), which
+// Compiled once per pair with -DXFA_HD=<64|128|256> -DXFA_DT=<bf16|f16> (see build.py), which
 // keeps the per-variant kernels in separate code objects (co-compiled template variants
 // perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
 #include "fmha_fwd_kernel.h"
-#include "fmha_fwd_pp_kernel.h"
 #include "fmha_decode_kernel.h"
 #include "fmha_launch.h"
 
@@ -43,21 +42,14 @@ template <int HD, typename T>
 static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
     dim3 grid(p.b * p.hk, p.num_splits / kDecWaves);
-    // GQA groups of <= 16 query rows run the 16x16x32 tile (fmha_decode_kernel.h, MR = 16)
-    const bool r16 = p.seqlen_q * p.group <= 16 && options().fwd_decode16;
-    if (p.kv_fp8) {
-        if (r16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
-        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
-    } else {
-        if (r16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
-        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
-    }
+    if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+    else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
 }
 
-template <int HD, typename T, int NW, bool PP>
+template <int HD, typename T, int NW>
 static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     const bool mask = p.wl >= 0 || p.wr >= 0;
     // FEAT: per-score transforms (ALiBi, softcap) and the paged / fp8 staging paths
@@ -68,43 +60,25 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     FwdParams pp = p;
     pp.n_mblocks = n_mb;
     pp.persistent = 0;
-    if (!PP && options().fwd_persistent > 0) {
+    if (p.persist_per_cu > 0) {
         const int items = p.b * p.hk * n_mb;
-        const int slots = options().num_cus * options().fwd_persistent;
+        const int slots = p.num_cus * p.persist_per_cu;
         if (items > slots) {
-            pp.persistent = p.work_ctr ? 3 : (options().fwd_order == 1 && slots % 8 == 0) ? 2 : 1;
-            pp.xcd_queues = p.work_ctr && options().fwd_xcdq && slots % 8 == 0 && p.b * p.hk >= 8;
+            pp.persistent = p.work_ctr ? 3 : (p.order == 1 && slots % 8 == 0) ? 2 : 1;
+            pp.xcd_queues = p.work_ctr && p.xcdq && slots % 8 == 0 && p.b * p.hk >= 8;
             grid = dim3(slots, 1, grid.z);
         }
     }
-    const size_t smem = PP ? (size_t)(4 * kBlockN * HD * 2 + 256 * HD * 2) : (size_t)(fwd_nbuf(HD) * 2 * kBlockN * HD * 2);
-    void (*kern)(const FwdParams);
-    if constexpr (PP) {
-        const int sm = options().fwd_sched;
-        if (!feat && sm == 1) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 1> : fmha_fwd_pp_kernel<HD, T, false, false, 1>;
-        else if (!feat && sm == 2) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 2> : fmha_fwd_pp_kernel<HD, T, false, false, 2>;
-        else if (!feat && sm == 3) kern = mask ? fmha_fwd_pp_kernel<HD, T, true, false, 3> : fmha_fwd_pp_kernel<HD, T, false, false, 3>;
-        else kern = mask ? (feat ? fmha_fwd_pp_kernel<HD, T, true, true> : fmha_fwd_pp_kernel<HD, T, true, false>)
-                         : (feat ? fmha_fwd_pp_kernel<HD, T, false, true> : fmha_fwd_pp_kernel<HD, T, false, false>);
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    } else {
-        kern = mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
-                    : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
-    }
-    static bool attr_done = false;   // benign race: idempotent attribute set
-    if (!attr_done) {
-        if constexpr (PP) {
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_pp_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        } else {
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-            (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        }
-        attr_done = true;
+    const size_t smem = (size_t)(fwd_nbuf(HD) * 2 * kBlockN * HD * 2);
+    void (*kern)(const FwdParams) =
+        mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
+             : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
+    static std::atomic<unsigned long long> attr_done{0};
+    if (first_on_device(attr_done, p.device)) {
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     }
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
@@ -114,13 +88,12 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
 #if XFA_HD > 128
-    // D = 256: 4-wave register-staged kernel only (no decode / ping-pong / DMA pipeline)
-    return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
+    // D = 256: 4-wave register-staged kernel only (no decode / DMA pipeline)
+    return launch_fwd_nw<XFA_HD, elem_t, 4>(p, st);
 #else
     if (p.decode) return launch_decode<XFA_HD, elem_t>(p, st);
-    if (options().fwd_pp && !p.kv_fp8) return launch_fwd_nw<XFA_HD, elem_t, 8, true>(p, st);
-    if (options().fwd_waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8, false>(p, st);
-    return launch_fwd_nw<XFA_HD, elem_t, 4, false>(p, st);
+    if (p.waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8>(p, st);
+    return launch_fwd_nw<XFA_HD, elem_t, 4>(p, st);
 #endif
 }
 

@@ -270,7 +270,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     };
     // P = exp2(S c - m c) -> T (the B operand of the PV product) for values [v0, v0 + n);
     // the row sum accumulates the rounded P pairs (v_dot2c against ones, two chains): the
-    // normaliser is then exactly the sum of the weights the PV MFMA multiplies.
+    // normaliser is then exactly the sum of the weights the PV MFMA multiplies.  (The reference
+    // sums the fp32 P, softmax_hip.h:129-189; the two normalisers differ by at most the bf16
+    // unit roundoff 2^-9 relative, so the LSE by at most 1.95e-3.  An fp32 sum beside the
+    // QK^T MFMAs was measured: it spills at 256 VGPRs and costs 27 % of C2 throughput.)
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef typename DT<T>::v2 T2;
     auto exp_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], const f2 m2, float (&rs)[2],
@@ -576,8 +579,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
 #pragma unroll
                     for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
                 }
-                // row sum of the rounded P_j weights (the normaliser is exactly the sum of the
-                // weights the PV MFMA multiplies): 16 pairs over the NPV MFMAs
+                // row sum of the rounded P_j weights: 16 pairs over the NPV MFMAs
                 constexpr int PPM = 16 / NPV;     // P pairs per PV MFMA
 #pragma unroll
                 for (int u = 0; u < PPM; ++u) {
@@ -669,9 +671,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     }
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
               (int64_t)(q_off + pos) * p.o_row + (int64_t)head * p.o_head;
-    if (p.dbg & 4) return;                 // timing experiment: no O / LSE stores
-    if (p.store8) store_o_row8<T, ND>(orow, acc_o, inv, p.d, hh);
-    else store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
+    store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
     if (p.lse && hh == 0) {
         p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] =
             empty ? INFINITY : (m_sc + __log2f(l_full)) * kLn2;

@@ -6,28 +6,25 @@
 
 #include "fmha_common.h"
 
+#include <atomic>
+
 namespace xfa {
 
-// Tuning knobs, settable through fmha_set_option() (used for in-process A/B runs).
+// Tuning knobs, settable through fmha_set_option() (schedule choices with equal results; the
+// parity suite runs under any of them via XFA_TEST_OPTIONS).  Atomic: a launch on another
+// thread reads each knob once, as a whole value.
 struct Options {
-    int fwd_waves = 8;        // waves per forward workgroup (4 or 8); 32 query rows per wave
-    int fwd_prio = 0;         // static s_setprio 1 for the younger half of the workgroup
-    int fwd_pp = 0;           // 1: ping-pong forward schedule (8 waves, fmha_fwd_pp_kernel.h)
-    int fwd_sched = 0;        // sched_group_barrier interleave bits (experiment knob)
-    int fwd_store8 = 0;       // legacy 8-byte O stores (A/B knob)
-    int fwd_persistent = 1;   // persistent grid (workgroups per CU; 0 = one workgroup per item)
-    int fwd_slack = 8;        // deferred rescale: running max may lag by this many log2 units
-    int fwd_order = 1;        // persistent item order: 0 boustrophedon, 1 XCD-grouped pairs
-    int fwd_dyn = 1;          // dynamic item queue: 0 never, 1 varlen only, 2 every persistent launch
-    int fwd_xcdq = 1;         // dynamic queue kind: 1 one unit-major queue per XCD, 0 one global
-                              // heaviest-row-block-first queue
-    int fwd_pipe = 1;         // software-pipelined loop over the unmasked key tiles
-    int fwd_dbg = 0;          // timing experiments only (results invalid when set)
-    int fwd_decode = 1;       // split-KV decode kernel when seqlen_q * H/Hk <= 32
-    int bwd_prio = 0;         // backward: static s_setprio 1 for the younger half (A/B)
-    int dec_wg_per_cu = 2;    // decode split target: workgroups per CU over all (b, kv head)
-    int fwd_decode16 = 0;     // 16x16x32 decode tile when seqlen_q * H/Hk <= 16 (slower on C5: A/B knob)
-    int num_cus = 256;        // filled by the C ABI from the device
+    std::atomic<int> fwd_waves{8};       // waves per forward workgroup (4 or 8); 32 query rows per wave
+    std::atomic<int> fwd_prio{0};        // static s_setprio 1 for the younger half of the workgroup
+    std::atomic<int> fwd_persistent{1};  // persistent grid (workgroups per CU; 0 = one workgroup per item)
+    std::atomic<int> fwd_slack{8};       // deferred rescale: running max may lag by this many log2 units
+    std::atomic<int> fwd_order{1};       // persistent item order: 0 boustrophedon, 1 XCD-grouped pairs
+    std::atomic<int> fwd_dyn{1};         // dynamic item queue: 0 never, 1 varlen only, 2 every persistent launch
+    std::atomic<int> fwd_xcdq{1};        // dynamic queue kind: 1 one unit-major queue per XCD, 0 one global
+                                         // heaviest-row-block-first queue
+    std::atomic<int> fwd_pipe{1};        // software-pipelined loop over the unmasked key tiles
+    std::atomic<int> fwd_decode{1};      // split-KV decode kernel when seqlen_q * H/Hk <= 32
+    std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
 };
 Options& options();
 
@@ -65,12 +62,9 @@ hipError_t launch_append(const AppendParams& p, bool fp16, hipStream_t st);
 
 // D = 256 (bucket of 129..256): 4 waves x 32 rows, one wave per SIMD (512 registers:
 // Q fragments and the O accumulator alone are 192), no LDS-DMA pipeline
-inline int fwd_block_m(int d) {
-    if (d > 128) return 128;
-    return options().fwd_pp ? 256 : options().fwd_waves * 32;
-}
-inline int fwd_num_m_blocks(int seqlen_q, int group, int d) {
-    return (seqlen_q * group + fwd_block_m(d) - 1) / fwd_block_m(d);
+inline int fwd_block_m(int d, int waves) { return d > 128 ? 128 : waves * 32; }
+inline int fwd_num_m_blocks(int seqlen_q, int group, int d, int waves) {
+    return (seqlen_q * group + fwd_block_m(d, waves) - 1) / fwd_block_m(d, waves);
 }
 
 }  // namespace xfa

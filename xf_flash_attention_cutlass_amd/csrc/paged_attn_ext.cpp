@@ -399,6 +399,23 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
     return {out, softmax_lse};
 }
 
+// Gradient outputs (export.cpp:1037-1060): a caller-given tensor must match q/k/v in dtype,
+// device and shape; a non-contiguous one is computed into a contiguous temporary and copied
+// back by grad_writeback.
+static at::Tensor grad_out(c10::optional<at::Tensor>& t, const at::Tensor& like) {
+    if (t.has_value()) {
+        const at::Tensor& x = t.value();
+        TORCH_CHECK(x.dtype() == like.dtype(), "gradient must have the same dtype as its input");
+        CHECK_DEVICE(x);
+        TORCH_CHECK(x.sizes() == like.sizes(), "gradient has the wrong shape");
+        if (x.is_contiguous()) return x;
+    }
+    return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
+}
+static void grad_writeback(c10::optional<at::Tensor>& t, at::Tensor& g) {
+    if (t.has_value() && !t.value().is_same(g)) { t.value().copy_(g); g = t.value(); }
+}
+
 std::vector<at::Tensor>
 mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
         const at::Tensor& out, const at::Tensor& softmax_lse, c10::optional<at::Tensor>& dq_,
@@ -434,17 +451,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size);
     CHECK_SHAPE(dout, batch_size, seqlen_q, num_heads, head_size_og);
     CHECK_SHAPE(softmax_lse, batch_size, num_heads, seqlen_q);
-    auto alloc = [&](c10::optional<at::Tensor>& t, const at::Tensor& like) {
-        if (t.has_value()) {
-            auto x = t.value();
-            TORCH_CHECK(x.dtype() == q.dtype(), "gradient must have the same dtype as q");
-            CHECK_DEVICE(x);
-            TORCH_CHECK(x.sizes() == like.sizes(), "gradient has the wrong shape");
-            if (x.is_contiguous()) return x;
-        }
-        return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
-    };
-    at::Tensor dq = alloc(dq_, q), dk = alloc(dk_, k), dv = alloc(dv_, v);
+    at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
     at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
@@ -453,7 +460,8 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
     auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
     auto lse = softmax_lse.contiguous();
-    const size_t ws = fmha_bwd_workspace_size(seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, head_size);
+    const size_t ws = fmha_bwd_workspace_size(seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k,
+                                              head_size, deterministic);
     at::Tensor workspace = torch::empty({(int64_t)ws}, opts.dtype(torch::kUInt8));
     if (seqlen_q > 0) {
         fmha_bwd(dout_padded.data_ptr(), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(), oc.data_ptr(),
@@ -466,10 +474,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     } else {
         dk.zero_(); dv.zero_(); softmax_d.zero_();
     }
-    auto fix = [&](c10::optional<at::Tensor>& t, at::Tensor& g) {
-        if (t.has_value() && !t.value().is_same(g)) { t.value().copy_(g); g = t.value(); }
-    };
-    fix(dq_, dq); fix(dk_, dk); fix(dv_, dv);
+    grad_writeback(dq_, dq); grad_writeback(dk_, dk); grad_writeback(dv_, dv);
     if (head_size_og % 8 != 0) {
         using torch::indexing::Slice; using torch::indexing::None;
         dq = dq.index({"...", Slice(None, head_size_og)});
@@ -505,11 +510,11 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     if (window_size_left >= max_seqlen_k) window_size_left = -1;
     if (window_size_right >= max_seqlen_k) window_size_right = -1;
     CHECK_SHAPE(softmax_lse, num_heads, total_q);
-    auto alloc = [&](c10::optional<at::Tensor>& t, const at::Tensor& like) {
-        if (t.has_value() && t.value().is_contiguous()) return t.value();
-        return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
-    };
-    at::Tensor dq = alloc(dq_, q), dk = alloc(dk_, k), dv = alloc(dv_, v);
+    CHECK_SHAPE(k, total_k, num_heads_k, head_size);
+    CHECK_SHAPE(v, total_k, num_heads_k, head_size);
+    CHECK_SHAPE(out, total_q, num_heads, head_size);
+    CHECK_SHAPE(dout, total_q, num_heads, head_size_og);
+    at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
     at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
@@ -518,17 +523,20 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
     auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
     auto lse = softmax_lse.contiguous();
-    const size_t ws = fmha_varlen_bwd_workspace_size(total_q, total_k, batch_size, num_heads, num_heads_k, head_size);
+    const size_t ws = fmha_varlen_bwd_workspace_size(total_q, max_seqlen_k, batch_size, num_heads,
+                                                     num_heads_k, head_size, deterministic);
     at::Tensor workspace = torch::empty({(int64_t)ws}, opts.dtype(torch::kUInt8));
     fmha_varlen_bwd(dout_padded.data_ptr(), qc.data_ptr(), kc.data_ptr(), vc.data_ptr(),
                     oc.data_ptr(), lse.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                     cu_seqlens_q.data_ptr(), cu_seqlens_k.data_ptr(),
                     alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs, max_seqlen_q,
                     max_seqlen_k, total_q, total_k, batch_size, num_heads, num_heads_k, head_size,
-                    softmax_scale, window_size_left, window_size_right, softcap,
-                    q.dtype() == torch::kFloat16, cur_stream(), workspace.data_ptr(), ws);
+                    softmax_scale, window_size_left, window_size_right, softcap, deterministic,
+                    q.dtype() == torch::kFloat16, cur_stream(), workspace.data_ptr(), ws,
+                    softmax_d.data_ptr());
     raise_if_failed("varlen_bwd");
-    (void)zero_tensors; (void)deterministic;
+    (void)zero_tensors;
+    grad_writeback(dq_, dq); grad_writeback(dk_, dk); grad_writeback(dv_, dv);
     if (head_size_og % 8 != 0) {
         using torch::indexing::Slice; using torch::indexing::None;
         dq = dq.index({"...", Slice(None, head_size_og)});

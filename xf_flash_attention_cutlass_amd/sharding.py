@@ -8,7 +8,8 @@ RCCL) that assembles the sharded outputs on every rank:
 
   * dense fwd/bwd (C2/C3)  : shard heads in contiguous, GQA-aligned ranges (a K/V head and all
                              query heads that read it stay on one rank, so dK/dV need no
-                             cross-rank reduction); fall back to batch shards when hk < world;
+                             cross-rank reduction); batch shards when there are fewer kv heads
+                             than ranks (then every rank needs at least one batch element);
   * varlen (C4)            : shard whole sequences, greedy-balanced on sum(s_q * s_k);
   * paged decode (C5)      : shard the batch; every rank owns its sequences' pages, no KV moves.
 """
@@ -73,38 +74,81 @@ def _world():
 
 def all_gather_heads(local: torch.Tensor, shards: List[Tuple[Shard, Shard]], head_dim: int = 2):
     """Assemble [b, s, H, d] from per-rank head shards [b, s, H_r, d] (all ranks get the full
-    tensor).  Uneven shards are padded to the largest for one all_gather_into_tensor."""
+    tensor)."""
+    return all_gather_dim(local, [q.size for q, _ in shards], head_dim)
+
+
+def _slice_alibi(alibi, heads: Shard | None = None, batch: Shard | None = None):
+    """ALiBi slopes ([H] or [b, H]) restricted to a rank's query heads / batch rows."""
+    if alibi is None:
+        return None
+    if heads is not None:
+        alibi = alibi[..., heads.start:heads.stop]
+    if batch is not None and alibi.dim() == 2:
+        alibi = alibi[batch.start:batch.stop]
+    return alibi.contiguous()
+
+
+def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
+    """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank:
+    one all_gather_into_tensor of pieces padded to the largest, then a narrow per rank."""
     dist, rank, world = _world()
     if world == 1:
         return local
-    hmax = max(q.size for q, _ in shards)
-    pad = list(local.shape)
-    pad[head_dim] = hmax
-    buf = local.new_zeros(pad)
-    buf.narrow(head_dim, 0, local.shape[head_dim]).copy_(local)
-    gathered = local.new_empty([world * pad[0]] + pad[1:])     # rank-major concatenation
-    dist.all_gather_into_tensor(gathered, buf.contiguous())
-    gathered = gathered.view([world] + pad)
-    pieces = [gathered[r].narrow(head_dim, 0, shards[r][0].size) for r in range(world)]
-    return torch.cat(pieces, dim=head_dim)
+    nmax = max(sizes)
+    shape = list(local.shape)
+    shape[dim] = nmax
+    buf = local.new_zeros(shape)
+    buf.narrow(dim, 0, local.shape[dim]).copy_(local)
+    buf = buf.movedim(dim, 0).contiguous()
+    gathered = local.new_empty([world * nmax] + list(buf.shape[1:]))   # rank-major
+    dist.all_gather_into_tensor(gathered, buf)
+    gathered = gathered.view([world, nmax] + list(buf.shape[1:]))
+    pieces = [gathered[r, :sizes[r]] for r in range(world)]
+    return torch.cat(pieces, dim=0).movedim(0, dim)
 
 
 def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
                       local_fn: Callable | None = None, gather: bool = True, **kw):
-    """Head-sharded attention: every rank holds the full (replicated) q/k/v views, computes
-    its GQA-aligned head range with `local_fn` (default: the gfx950 kernels) and, if `gather`,
-    all-gathers the outputs.  Returns (out, my_query_head_shard)."""
+    """Dense attention sharded over ranks: every rank holds the full (replicated) q/k/v views,
+    computes its GQA-aligned query-head range with `local_fn` (default: the gfx950 kernels)
+    and, if `gather`, all-gathers the outputs.  With fewer kv heads than ranks the batch is
+    sharded instead.  ALiBi slopes in `kw` are sliced to the rank's heads / batch rows.
+    Returns (out, my shard) where the shard is a query-head range, or a batch range
+    (`Shard` with `.batch = True` semantics: see `attention_shards`)."""
     dist, rank, world = _world()
     if local_fn is None:
         from . import flash_attn_func as local_fn
-    shards = head_shards(q.shape[2], k.shape[2], world)
-    qs, ks = shards[rank]
-    out_local = local_fn(q[:, :, qs.start:qs.stop].contiguous(),
-                         k[:, :, ks.start:ks.stop].contiguous(),
-                         v[:, :, ks.start:ks.stop].contiguous(), **kw)
+    kind, shards = attention_shards(q.shape[0], q.shape[2], k.shape[2], world)
+    alibi = kw.pop("alibi_slopes", None)
+    if kind == "heads":
+        qs, ks = shards[rank]
+        if alibi is not None:
+            kw["alibi_slopes"] = _slice_alibi(alibi, heads=qs)
+        out_local = local_fn(q[:, :, qs.start:qs.stop].contiguous(),
+                             k[:, :, ks.start:ks.stop].contiguous(),
+                             v[:, :, ks.start:ks.stop].contiguous(), **kw)
+        if not gather:
+            return out_local, qs
+        return all_gather_dim(out_local, [a.size for a, _ in shards], 2), qs
+    bs = shards[rank]
+    if alibi is not None:
+        kw["alibi_slopes"] = _slice_alibi(alibi, batch=bs)
+    out_local = local_fn(q[bs.start:bs.stop].contiguous(), k[bs.start:bs.stop].contiguous(),
+                         v[bs.start:bs.stop].contiguous(), **kw)
     if not gather:
-        return out_local, qs
-    return all_gather_heads(out_local, shards), qs
+        return out_local, bs
+    return all_gather_dim(out_local, [s.size for s in shards], 0), bs
+
+
+def attention_shards(batch: int, num_heads: int, num_heads_k: int, world: int):
+    """("heads", [(q heads, kv heads)] per rank) when every rank gets at least one kv head,
+    else ("batch", [batch range] per rank)."""
+    if num_heads_k >= world:
+        return "heads", head_shards(num_heads, num_heads_k, world)
+    if batch < world:
+        raise ValueError(f"cannot shard {num_heads_k} kv heads or {batch} batch rows over {world} ranks")
+    return "batch", batch_shards(batch, world)
 
 
 def sharded_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, local_fn: Callable | None = None,
@@ -156,3 +200,29 @@ def sharded_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, local_fn: Callable | Non
 def batch_shards(batch: int, world: int) -> List[Shard]:
     """Paged decode (C5): contiguous batch ranges; each rank owns its sequences' KV pages."""
     return even_ranges(batch, world)
+
+
+def sharded_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                   cache_seqlens: torch.Tensor, block_table: torch.Tensor,
+                   local_fn: Callable | None = None, gather: bool = True, **kw):
+    """Batch-sharded paged decode (C5): rank r takes batch rows `batch_shards(b, world)[r]` of
+    q / cache_seqlens / block_table; the page pools stay where they are (a rank only reads the
+    pages its own rows point to, so in a deployment each rank holds just its sequences'
+    pages).  Outputs [b, sq, H, d] are all-gathered in batch order.  Returns (out, my rows)."""
+    dist, rank, world = _world()
+    if local_fn is None:
+        from . import flash_attn_with_kvcache
+
+        def local_fn(qq, kc, vc, sl, bt, **kk):
+            return flash_attn_with_kvcache(qq, kc, vc, cache_seqlens=sl, block_table=bt, **kk)
+    shards = batch_shards(q.shape[0], world)
+    bs = shards[rank]
+    alibi = kw.pop("alibi_slopes", None)
+    if alibi is not None:
+        kw["alibi_slopes"] = _slice_alibi(alibi, batch=bs)
+    out_local = local_fn(q[bs.start:bs.stop].contiguous(), kcache, vcache,
+                         cache_seqlens[bs.start:bs.stop].contiguous(),
+                         block_table[bs.start:bs.stop].contiguous(), **kw)
+    if not gather:
+        return out_local, bs
+    return all_gather_dim(out_local, [s.size for s in shards], 0), bs
