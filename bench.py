@@ -2,21 +2,33 @@
 
 Workloads (BASELINE.json configs):
   --mode fwd     (default) C2: mha_fwd B=4 H=32 S=4096 D=128 bf16 causal; one step = one
-                 forward over the batch.  The line also carries a short C3 (fwd+bwd) sample
-                 under "fwd_bwd" because the metric names both.
+                 forward over the batch.  The default line also carries driver-timed
+                 sub-results for C3 ("fwd_bwd"), C4 ("varlen") and C5 ("decode"), each with its
+                 own roofline, because the metric names fwd and fwd+bwd and BASELINE lists all.
   --mode fwdbwd  C3: mha_fwd + mha_bwd, same shape (FLOPs = 3.5 x fwd, the usual convention).
   --mode varlen  C4: mha_varlen_fwd, 32 ragged sequences, total 131072 tokens, H=32 D=128 bf16.
   --mode decode  C5: paged-KV decode (fwd_kvcache), per GPU B=8 H=32 Hk=8 Sq=1, cache 32768
                  tokens, page 16, fp8 e4m3fn K/V; HBM-bound, reported in GB/s.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fwd|fwdbwd|varlen|decode]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ...] [--scaling weak|strong]
 
-N > 1 is launched by torch.distributed.run (one process per GPU): every rank owns its own
-shard of independent (batch, head) / sequence units — attention has no cross-unit reduction,
-so the timed region has no collective ("scaling": "weak"); the RCCL all-gather of outputs
-over xGMI that assembles the sharded result is timed separately under "allgather".
+Multi-GPU (one process per GPU, RCCL = torch.distributed "nccl" over xGMI).  With --gpus N > 1
+and no WORLD_SIZE in the environment this process is only a launcher: before touching the GPU
+it starts `python -m torch.distributed.run --nproc-per-node N` on this same file as a CHILD
+process and exits with its status (the driver may also launch the ranks itself).  Sharding
+(sharding.py; attention has no cross-unit reduction in the forward, so no collective sits in
+the timed step):
+  --scaling weak   (default) every rank owns a batch shard of the same per-GPU size: the global
+                   batch is N x the single-GPU config (C2/C3: 4N sequences, C4: 32N sequences,
+                   C5: 8N sequences, each rank holding its own sequences' pages);
+  --scaling strong the global problem is the single-GPU config (C5: the survey's global B=64):
+                   C2/C3 shard GQA-aligned head ranges (H/N heads per rank), C4 whole sequences
+                   balanced on sum(s^2), C5 batch rows (64/N per rank).
+The RCCL all-gather that assembles the sharded output on every rank is timed separately
+("allgather", with "value_with_gather").  value = units processed by ALL ranks / max-over-ranks
+wall time of exactly K steps between barriers.
 
-Prints ONE JSON line on rank 0 (value = whole-job throughput summed over all ranks).
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -25,6 +37,8 @@ import glob
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,31 +57,41 @@ def fwd_flops(b, h, sq, sk, d, causal):
     return f / 2 if causal else f
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["fwd", "fwdbwd", "varlen", "decode"], default="fwd")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--batch", type=int, default=0, help="default: 4 (fwd), 8 (decode)")
     ap.add_argument("--heads", type=int, default=32)
     ap.add_argument("--seqlen", type=int, default=0, help="default: 4096 (fwd), 32768 (decode)")
     ap.add_argument("--headdim", type=int, default=128)
     ap.add_argument("--no-causal", action="store_true")
     ap.add_argument("--ragged", action="store_true", help="decode: cache lengths U[1, S]")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="input sets cycled step by step (default: 2 for fwd/fwdbwd, so every "
+                         "step reads inputs last touched two steps ago; C4/C5 inputs exceed the "
+                         "256 MiB Infinity Cache on their own)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the fwd_bwd sample")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the C3/C4/C5 sub-results of the default (fwd) line")
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="replay one step as a captured hipGraph")
     ap.add_argument("--opt", action="append", default=[],
-                    help="name=value tuning option (fmha_set_option) for A/B runs")
+                    help="name=value schedule knob (fmha_set_option) for A/B runs; recorded in "
+                         "the line")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed seconds of steps before the warmup (GPU clock ramp)")
-    return ap.parse_args()
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="launcher/aggregation self-test on CPU (gloo, a tiny matmul step): "
+                         "NOT a benchmark; used by tests/test_bench_launcher.py")
+    return ap.parse_args(argv)
 
 
-# ----------------------------------------------------------------------------- CPU baselines
+# ----------------------------------------------------------------------------- host info
 def _threads():
     t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     torch.set_num_threads(t)
@@ -75,6 +99,13 @@ def _threads():
 
 
 def _host():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
     return platform.processor() or platform.machine()
 
 
@@ -137,75 +168,131 @@ def varlen_lengths(n=32, total=131072, lo=1024, hi=7168, seed=0):
     return [int(x) for x in lens]
 
 
-def build_workload(a, dev, rank):
-    """Returns dict(step, units, bound, config, cpu, out) for the selected mode; `units` is
-    the algorithmic FLOPs (mfma-bound) or bytes (hbm-bound) one step processes."""
-    import xf_flash_attention_cutlass_amd as xfa
+def _set_options(opts):
     from xf_flash_attention_cutlass_amd import capi
-    for o in a.opt:                       # tuning knobs (fmha_set_option), A/B runs only
+    for o in opts:                       # schedule knobs (fmha_set_option), A/B runs only
         name, val = o.split("=")
         if capi.lib().fmha_set_option(name.encode(), int(val)) != 0:
             raise SystemExit(capi.lib().fmha_last_error().decode())
+
+
+def _rotating(sets):
+    """Step closure helper: returns next() cycling through the input sets."""
+    state = {"i": 0}
+
+    def nxt():
+        s = sets[state["i"] % len(sets)]
+        state["i"] += 1
+        return s
+    return nxt
+
+
+def workload_dense(a, mode, dev, rank, world):
+    """C2 (mode fwd) / C3 (mode fwdbwd).  weak: B per rank; strong: this rank's head shard."""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import sharding
+    pa = xfa.paged_attn
+    B, S, H, D = a.batch or 4, a.seqlen or 4096, a.heads, a.headdim
+    causal = not a.no_causal
+    scale = D ** -0.5
+    Hr, shard = H, f"batch shard {B} of global {B * world}"
+    if a.scaling == "strong":
+        qs, _ = sharding.head_shards(H, H, world)[rank]
+        Hr, shard = qs.size, f"heads [{qs.start}, {qs.stop}) of {H}"
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    nrot = a.rotate or 2
+    sets = []
+    for _ in range(nrot):
+        q, k, v = (torch.randn(B, S, Hr, D, device=dev, dtype=torch.bfloat16, generator=g)
+                   for _ in range(3))
+        out = torch.empty_like(q)
+        dout = torch.randn_like(q)
+        sets.append((q, k, v, out, dout))
+    nxt = _rotating(sets)
+    res = {}
+
+    def fwd():
+        q, k, v, out, _ = nxt()
+        res["r"] = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
+
+    def fwdbwd():
+        q, k, v, out, dout = nxt()
+        r = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
+        pa.bwd(dout, q, k, v, out, r[5], None, None, None, None, 0.0, scale, causal, -1, -1,
+               0.0, False, None, None)
+        res["r"] = r
+
+    ff = fwd_flops(B, Hr, S, S, D, causal)
+    mult = 3.5 if mode == "fwdbwd" else 1.0
+    cs = "causal" if causal else "non-causal"
+    glob_b = B * world if a.scaling == "weak" else B
+    return dict(step=fwd if mode == "fwd" else fwdbwd, units=ff * mult, bound="mfma",
+                out=lambda: sets[0][3], gather_dim=0 if a.scaling == "weak" else 2,
+                config={"workload": f"mha_{mode} B={B} H={H} S={S} D={D} bf16 {cs}",
+                        "global_batch": glob_b, "seq_len": S, "heads": H, "head_dim": D,
+                        "rank_shard": shard, "input_sets": nrot,
+                        "parallelism": f"dp{world} ({a.scaling} scaling: "
+                                       f"{'batch' if a.scaling == 'weak' else 'GQA-aligned head'}"
+                                       f" shards, no collective in the step)"},
+                cpu=lambda: cpu_baseline_dense(8, S, D, causal, a.cpu_baseline_seconds))
+
+
+def workload_varlen(a, dev, rank, world):
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import sharding
     pa = xfa.paged_attn
     H, D = a.heads, a.headdim
     causal = not a.no_causal
     scale = D ** -0.5
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)   # each rank: its own shard
+    if a.scaling == "weak":
+        lens = varlen_lengths(seed=rank)        # every rank its own 32 sequences
+        shard = f"32 sequences of global {32 * world}"
+    else:
+        all_lens = varlen_lengths()
+        mine = sharding.balanced_sequences(all_lens, all_lens, world)[rank]
+        lens = [all_lens[i] for i in mine]
+        shard = f"sequences {mine}"
+    tot = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    q, k, v = (torch.randn(tot, H, D, device=dev, dtype=torch.bfloat16, generator=g)
+               for _ in range(3))
+    out = torch.empty_like(q)
+    mx = max(lens)
+
+    def step():
+        pa.varlen_fwd(q, k, v, out, cu, cu, None, None, None, mx, mx, 0.0, scale, False,
+                      causal, -1, -1, 0.0, False, None)
+
+    fl = sum(fwd_flops(1, H, s, s, D, causal) for s in lens)
     cs = "causal" if causal else "non-causal"
+    return dict(step=step, units=fl, bound="mfma", out=lambda: out, gather_dim=0,
+                config={"workload": f"mha_varlen_fwd 32 ragged seqs U[1024,7168] (seed 0) "
+                                    f"total=131072 H={H} D={D} bf16 {cs}",
+                        "global_batch": 32 * world if a.scaling == "weak" else 32,
+                        "seq_len": mx, "total_tokens": tot, "heads": H, "head_dim": D,
+                        "rank_shard": shard,
+                        "parallelism": f"dp{world} ({a.scaling} scaling: sequence shards, "
+                                       f"no collective)"},
+                cpu=lambda: cpu_baseline_dense(8, lens[0], D, causal, a.cpu_baseline_seconds))
 
-    if a.mode in ("fwd", "fwdbwd"):
-        B, S = a.batch or 4, a.seqlen or 4096
-        q, k, v = (torch.randn(B, S, H, D, device=dev, dtype=torch.bfloat16, generator=g)
-                   for _ in range(3))
-        out = torch.empty_like(q)
-        dout = torch.randn_like(q)
-        lse = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)[5]
 
-        def fwd():
-            pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
-
-        def fwdbwd():
-            r = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
-            pa.bwd(dout, q, k, v, out, r[5], None, None, None, None, 0.0, scale, causal, -1, -1,
-                   0.0, False, None, None)
-
-        ff = fwd_flops(B, H, S, S, D, causal)
-        mult = 3.5 if a.mode == "fwdbwd" else 1.0
-        return dict(step=fwd if a.mode == "fwd" else fwdbwd, units=ff * mult, bound="mfma",
-                    out=out, extra=(fwdbwd, ff * 3.5) if a.mode == "fwd" else None,
-                    config={"workload": f"mha_{a.mode} B={B} H={H} S={S} D={D} bf16 {cs}",
-                            "global_batch": B * a.world, "seq_len": S, "heads": H,
-                            "head_dim": D,
-                            "parallelism": f"dp{a.world} (batch x head shards, no collective "
-                                           f"in step)"},
-                    cpu=lambda: cpu_baseline_dense(8, S, D, causal, a.cpu_baseline_seconds))
-
-    if a.mode == "varlen":
-        lens = varlen_lengths()
-        tot = sum(lens)
-        cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32,
-                          device=dev)
-        q, k, v = (torch.randn(tot, H, D, device=dev, dtype=torch.bfloat16, generator=g)
-                   for _ in range(3))
-        out = torch.empty_like(q)
-        mx = max(lens)
-
-        def step():
-            pa.varlen_fwd(q, k, v, out, cu, cu, None, None, None, mx, mx, 0.0, scale, False,
-                          causal, -1, -1, 0.0, False, None)
-
-        fl = sum(fwd_flops(1, H, s, s, D, causal) for s in lens)
-        s0 = lens[0]
-        return dict(step=step, units=fl, bound="mfma", out=out, extra=None,
-                    config={"workload": f"mha_varlen_fwd {len(lens)} ragged seqs "
-                                        f"U[1024,7168] (seed 0) total={tot} H={H} D={D} bf16 "
-                                        f"{cs}", "global_batch": len(lens) * a.world,
-                            "seq_len": mx, "total_tokens": tot, "heads": H, "head_dim": D,
-                            "parallelism": f"dp{a.world} (sequence shards, no collective)"},
-                    cpu=lambda: cpu_baseline_dense(8, s0, D, causal, a.cpu_baseline_seconds))
-
-    # decode (C5)
-    B, S, HK, page = a.batch or 8, a.seqlen or 32768, 8, 16
+def workload_decode(a, dev, rank, world):
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import sharding
+    pa = xfa.paged_attn
+    H, D, HK, page = a.heads, a.headdim, 8, 16
+    S = a.seqlen or 32768
+    scale = D ** -0.5
+    if a.scaling == "weak":
+        B = a.batch or 8
+        shard = f"batch {B} of global {B * world}"
+        glob_b = B * world
+    else:
+        glob_b = a.batch or 64
+        bs = sharding.batch_shards(glob_b, world)[rank]
+        B = bs.size
+        shard = f"batch rows [{bs.start}, {bs.stop}) of {glob_b}"
     nblk_seq = S // page
     nblocks = B * nblk_seq
     if a.ragged:
@@ -214,9 +301,10 @@ def build_workload(a, dev, rank):
     else:
         lens = torch.full((B,), S, dtype=torch.int32)
     seqlens = lens.to(dev)
-    gp = torch.Generator().manual_seed(0)
+    gp = torch.Generator().manual_seed(rank)
     table = torch.randperm(nblocks, generator=gp).to(torch.int32).view(B, nblk_seq).to(dev)
     ks, vs = 1.0 / 16, 1.0 / 16
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
     kc = torch.empty(nblocks, page, HK, D, device=dev, dtype=torch.uint8)
     vc = torch.empty_like(kc)
     for c, sc_ in ((kc, ks), (vc, vs)):      # chunked to bound the bf16 temporary
@@ -233,14 +321,23 @@ def build_workload(a, dev, rank):
 
     step()
     nbytes = int(lens.sum()) * HK * D * 2 + 2 * B * H * D * 2 + table.numel() * 4 + B * 4
-    return dict(step=step, units=nbytes, bound="hbm", out=res["o"], extra=None,
-                config={"workload": f"paged-KV decode B={B} H={H} Hk={HK} Sq=1 "
+    return dict(step=step, units=nbytes, bound="hbm", out=lambda: res["o"], gather_dim=0,
+                config={"workload": f"paged-KV decode B={B}/GPU H={H} Hk={HK} Sq=1 "
                                     f"cache={'U[1,%d]' % S if a.ragged else S} page={page} "
                                     f"D={D} fp8-e4m3fn K/V (scale 1/16), q bf16",
-                        "global_batch": B * a.world, "seq_len": S, "heads": H, "head_dim": D,
-                        "parallelism": f"dp{a.world} (batch shards: each rank owns its "
-                                       f"sequences' pages, no collective)"},
+                        "global_batch": glob_b, "seq_len": S, "heads": H, "head_dim": D,
+                        "rank_shard": shard,
+                        "parallelism": f"dp{world} ({a.scaling} scaling: batch shards, each "
+                                       f"rank owns its sequences' pages, no collective)"},
                 cpu=lambda: cpu_baseline_decode(H, HK, S, D, min(a.cpu_baseline_seconds, 10)))
+
+
+def build_workload(a, mode, dev, rank, world):
+    if mode in ("fwd", "fwdbwd"):
+        return workload_dense(a, mode, dev, rank, world)
+    if mode == "varlen":
+        return workload_varlen(a, dev, rank, world)
+    return workload_decode(a, dev, rank, world)
 
 
 def measured_traffic(mode):
@@ -258,8 +355,9 @@ def measured_traffic(mode):
         return None
 
 
-def timed(step, steps, stream):
-    """Run `steps` steps with HIP events on the launch stream; returns mean event ms."""
+def event_ms(step, steps, stream):
+    """Mean per-step time from HIP events recorded on the launch stream around every step
+    (a separate pass: the event records do not sit in the wall-clock timed region)."""
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     for i in range(steps):
@@ -270,20 +368,132 @@ def timed(step, steps, stream):
     return sum(s.elapsed_time(e) for s, e in evs) / steps
 
 
-def main():
-    a = parse()
+def prewarm(step, seconds, sync):
+    """GPU clock ramp: an idle MI355X needs a few hundred ms of sustained load to reach its
+    steady clock (measured: 20 steps after 5 warmups read 12 % low on C2)."""
+    t = time.perf_counter()
+    while time.perf_counter() - t < seconds:
+        for _ in range(8):
+            step()
+        sync()
+
+
+def roofline(w, ms, mode):
+    hbm = w["bound"] == "hbm"
+    scale_u = 1e9 if hbm else 1e12
+    achieved = w["units"] / (ms / 1e3) / scale_u
+    peak = PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS
+    tr = measured_traffic(mode)
+    roof = {"bound": w["bound"], "achieved": round(achieved, 2), "peak": peak,
+            "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": tr["bytes"] if tr else None,
+            "algorithmic_per_launch": w["units"], "kernel_ms": round(ms, 4)}
+    if tr:
+        roof["traffic_source"] = tr["file"]
+    return roof
+
+
+def sub_result(a, mode, dev, stream):
+    """A driver-timed sub-result (same method as the main line, rank-local, 1 GPU)."""
+    w = build_workload(a, mode, dev, 0, 1)
+    step = w["step"]
+    prewarm(step, 0.5, torch.cuda.synchronize)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    k = max(10, a.steps)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) / k * 1e3
+    ev = event_ms(step, k, stream)
+    hbm = w["bound"] == "hbm"
+    u = 1e9 if hbm else 1e12
+    out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
+           "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
+           "unit": "GB/s" if hbm else "TFLOP/s", "roofline": roofline(w, ev, mode)}
+    del w
+    torch.cuda.empty_cache()
+    return out
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, argv):
+    """Start N ranks as a child `torch.distributed.run` on this file (this process has not
+    touched the GPU and never execs: it waits for the child and returns its status)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_cpu(a, rank, world):
+    """Launcher / barrier / max-over-ranks self-test on CPU with gloo (not a benchmark)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.randn(256, 256)
+    step = lambda: x @ x          # noqa: E731
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        units = 2.0 * 256 ** 3 * a.steps * world
+        print(json.dumps({"metric": "bench launcher self-test (CPU gloo; not a benchmark)",
+                          "value": round(units / t.item() / 1e9, 3), "unit": "GFLOP/s",
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": round(t.item() / a.steps * 1e3, 4),
+                          "world_size": world,
+                          "backend": dist.get_backend() if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with "
+                         f"--nproc-per-node {a.gpus} (or let bench.py launch the ranks)")
     a.world = world
+    if a.selftest_cpu:
+        return selftest_cpu(a, rank, world)
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+    _set_options(a.opt)
 
-    w = build_workload(a, dev, rank)
+    w = build_workload(a, a.mode, dev, rank, world)
     step = w["step"]
     # Optional: replay a captured hipGraph of one step (same kernels).  Measured on C5 decode
     # it is slower than eager launches on this stack (0.136 vs 0.129 ms per step), so eager
@@ -300,20 +510,11 @@ def main():
             step()
         torch.cuda.synchronize()
         step = graph.replay
-    # GPU clock ramp: an idle MI355X needs a few hundred ms of sustained load to reach its
-    # steady clock (measured: 20 steps after 5 warmups read 12 % low on C2).  Run the step
-    # untimed for --prewarm-s seconds before the W warmup steps; the timed region is still
-    # exactly K steps.
-    t_pw = time.perf_counter()
-    while time.perf_counter() - t_pw < a.prewarm_s:
-        for _ in range(8):
-            step()
-        torch.cuda.synchronize()
+    prewarm(step, a.prewarm_s, torch.cuda.synchronize)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    # Kernel-level timing with HIP events on the stream the kernels are launched on
-    # (paged_attn launches on torch's current stream).
+    # kernels launch on torch's current stream; HIP events go on that stream
     stream = torch.cuda.current_stream()
 
     if dist:
@@ -326,63 +527,56 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # kernel-level time per step (roofline "achieved"): a separate pass of K steps bracketed
-    # by HIP events on the launch stream, so the event records do not sit in the timed region
-    ev_ms = timed(step, a.steps, stream)
+    ev_ms = event_ms(step, a.steps, stream)
 
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    units = torch.tensor([w["units"]], device=dev, dtype=torch.float64)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+        dist.all_reduce(units, op=dist.ReduceOp.SUM)
+    elapsed, total_units = t.item(), units.item()
 
     hbm = w["bound"] == "hbm"
     scale_u = 1e9 if hbm else 1e12
-    value = w["units"] * a.steps * world / elapsed / scale_u
+    value = total_units * a.steps / elapsed / scale_u
     ms_per_step = elapsed / a.steps * 1e3
 
     allgather = None
     if dist:
-        out = w["out"]
-        # RCCL all-gather of every rank's O shard over xGMI (assembling the sharded output).
-        gathered = torch.empty((world * out.shape[0],) + tuple(out.shape[1:]), device=dev,
-                               dtype=out.dtype)
+        out = w["out"]()
+        gd = w["gather_dim"]
+        # RCCL all-gather of every rank's output shard over xGMI (assembling the full output)
+        from xf_flash_attention_cutlass_amd import sharding
+        n_local = torch.tensor([out.shape[gd]], device=dev)
+        sizes = [torch.zeros_like(n_local) for _ in range(world)]
+        dist.all_gather(sizes, n_local)
+        sizes = [int(s.item()) for s in sizes]
         for _ in range(3):
-            dist.all_gather_into_tensor(gathered, out)
+            sharding.all_gather_dim(out, sizes, gd)
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(10):
-            dist.all_gather_into_tensor(gathered, out)
+            full = sharding.all_gather_dim(out, sizes, gd)
         torch.cuda.synchronize()
         ag = torch.tensor([(time.perf_counter() - t1) / 10], device=dev, dtype=torch.float64)
         dist.all_reduce(ag, op=dist.ReduceOp.MAX)
         ag_ms = ag.item() * 1e3
-        allgather = {"ms": round(ag_ms, 3),
+        allgather = {"ms": round(ag_ms, 3), "gathered_shape": list(full.shape),
                      "bytes_per_rank_in": out.numel() * out.element_size() * (world - 1),
-                     "value_with_gather": round(w["units"] * world /
-                                                ((ms_per_step + ag_ms) / 1e3) / scale_u, 2)}
+                     "value_with_gather": round(total_units / ((ms_per_step + ag_ms) / 1e3)
+                                                / scale_u, 2)}
 
-    extra = None
-    if w["extra"] and not a.no_extras:
-        fn, units = w["extra"]
-        for _ in range(2):
-            fn()
-        torch.cuda.synchronize()
-        ms = timed(fn, max(10, a.steps // 2), stream)
-        extra = {"workload": "mha_fwd + mha_bwd (C3), same shape; FLOPs = 3.5 x fwd",
-                 "ms_per_step": round(ms, 4), "tflops": round(units / (ms / 1e3) / 1e12, 2),
-                 "frac": round(units / (ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    extras = {}
+    if rank == 0 and a.mode == "fwd" and world == 1 and not a.no_extras:
+        extras["fwd_bwd"] = sub_result(a, "fwdbwd", dev, stream)
+        extras["varlen"] = sub_result(a, "varlen", dev, stream)
+        extras["decode"] = sub_result(a, "decode", dev, stream)
+    if dist:
+        dist.barrier()
 
     if rank == 0:
-        achieved = w["units"] / (ev_ms / 1e3) / scale_u
-        peak = PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS
-        tr = measured_traffic(a.mode)
-        roof = {"bound": w["bound"], "achieved": round(achieved, 2), "peak": peak,
-                "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": tr["bytes"] if tr else None,
-                "algorithmic_per_launch": w["units"], "kernel_ms": round(ev_ms, 4)}
-        if tr:
-            roof["traffic_source"] = tr["file"]
+        from xf_flash_attention_cutlass_amd import capi
         line = {
             "metric": METRIC if not hbm else "paged-KV decode HBM GB/s (C5)",
             "value": round(value, 2),
@@ -392,17 +586,20 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "bf16" if not hbm else "fp8-e4m3 K/V, bf16 q/o, f32 accumulate",
             "data": "synthetic (torch.randn, N(0,1)), inputs resident in HBM",
             "prewarm_s": a.prewarm_s,
             "launch": "hipGraph replay of one step" if use_graph else "eager",
+            "options": dict(o.split("=") for o in a.opt),
+            "library": capi.lib().fmha_version().decode(),
             "config": w["config"],
-            "roofline": roof,
+            "roofline": roofline(w, ev_ms, a.mode),
         }
-        if extra:
-            line["fwd_bwd"] = extra
+        if dist:
+            line["rccl"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+        line.update(extras)
         if allgather:
             line["allgather"] = allgather
         if world == 1 and not a.no_cpu_baseline:
@@ -410,7 +607,8 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

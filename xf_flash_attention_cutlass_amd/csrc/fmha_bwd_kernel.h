@@ -44,8 +44,9 @@ template <int HD> constexpr size_t bwd_smem_bytes() {
 // dQ partial sums -> the fp32 accumulator: float atomics into one [rows][HD] accumulator, or
 // (deterministic) plain stores into this key block's own slice, summed in key-block order by
 // the convert kernel
-__device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off, bool det) {
-    if (det) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+template <bool DET>
+__device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
+    if constexpr (DET) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
     else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
 }
 constexpr int kBwdBlockM = 32;               // query rows per tile
@@ -172,7 +173,9 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
 }
 
 // ---------------------------------------------------------------- main ---------------------
-template <int HD, typename T, bool MASK, bool FEAT>
+// DET (deterministic dQ slices) is instantiated only with MASK = FEAT = true, whose runtime
+// tests cover every window / feature combination.
+template <int HD, typename T, bool MASK, bool FEAT, bool DET = false>
 __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
     using V8 = typename DT<T>::v8;
     constexpr int NW = bwd_waves<HD>();
@@ -379,8 +382,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
-    const bool det = p.dq_slices > 0;
-    float* const dq_base = p.dq_accum + (det ? (int64_t)blockIdx.y * p.acc_slice : 0);
+    float* const dq_base = p.dq_accum + (DET ? (int64_t)blockIdx.y * p.acc_slice : 0);
     float lsd_cur = 0.f;
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible
@@ -537,7 +539,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 const int base = d < p.d ? (16 * mt + 4 * g16) * arow + d * 4 : kOOB;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    dq_add(dq[i][r], qrs, base + r * arow, det);
+                    dq_add<DET>(dq[i][r], qrs, base + r * arow);
             }
         }
         __syncthreads();
