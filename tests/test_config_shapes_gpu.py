@@ -4,8 +4,7 @@ Each test runs the HIP path at exactly the benched shape, then checks sampled (b
 sequence slices against the pinned CPU oracle with the reference's own rules (test.py:975 fwd,
 :984-986 gradients, :1593-1594 kvcache; LSE within 1e-3), and covers the rest of the output
 with size-independent properties (bitwise equality with another schedule of the same kernel).
-LSE gates: 2^-9 for the general forward (its normaliser sums the rounded P weights: see
-test_fwd_gpu.py), 1e-3 for the decode kernel (fp32 sum).
+LSE gate: 1e-3 absolute (fp32 intermediates).
 Per-case max|err| and the bound are collected into the parity report (XFA_PARITY_REPORT).
 
   C2  mha_fwd  B4 H32 S4096 D128 bf16 causal (persistent XCD-paired schedule, 512 items)
@@ -22,8 +21,8 @@ from oracle import attention_ref as orc
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-LSE_ATOL = 2.0 ** -9        # general forward (rounded-P normaliser)
-LSE_ATOL_DEC = 1e-3         # decode kernel (fp32 P sum)
+LSE_ATOL = 1e-3
+LSE_ATOL_DEC = 1e-3
 
 
 @pytest.fixture(scope="module")

@@ -3,11 +3,8 @@
 Pass rule = the reference's own (test.py:975, 1296, 1593-1594): max|out - out_ref| must be at
 most 2x (fwd, varlen) or 3x + 1e-5 (kvcache) the error of the low-precision PyTorch path
 max|out_pt - out_ref|.  LSE (fp32) is checked against the fp32 log-sum-exp of the oracle
-(oracle.attention_lse_ref) with an absolute tolerance of 2^-9 = 1.95e-3: the kernel's
-normaliser is the sum of the bf16/fp16-ROUNDED P weights that the PV MFMA multiplies (the
-reference sums the fp32 P), and rounding each weight to 8 significant bits moves the sum by at
-most 2^-9 relative, i.e. the LSE by at most 2^-9 absolute.  (The decode kernel sums fp32 P and
-is held to 1e-3.)
+(oracle.attention_lse_ref) with an absolute tolerance of 1e-3 (fp32 intermediates
+within 1e-3; the kernels sum the fp32 P as the reference's softmax does).
 """
 import math
 
@@ -19,7 +16,7 @@ from tests import golden_util as gu
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-LSE_ATOL = 2.0 ** -9
+LSE_ATOL = 1e-3
 
 
 @pytest.fixture(scope="module")

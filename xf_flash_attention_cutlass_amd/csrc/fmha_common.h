@@ -169,10 +169,6 @@ template <> struct DT<__bf16> {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
     }
     typedef __attribute__((ext_vector_type(2))) __bf16 v2;
-    // acc + a.x + a.y (v_dot2c_f32_bf16 against ones)
-    static __device__ __forceinline__ float sum2(const v2& a, float acc) {
-        return __builtin_amdgcn_fdot2_f32_bf16(a, v2{(__bf16)1.f, (__bf16)1.f}, acc, false);
-    }
 };
 template <> struct DT<_Float16> {
     typedef f16x8 v8;
@@ -180,9 +176,6 @@ template <> struct DT<_Float16> {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
     }
     typedef __attribute__((ext_vector_type(2))) _Float16 v2;
-    static __device__ __forceinline__ float sum2(const v2& a, float acc) {
-        return __builtin_amdgcn_fdot2(a, v2{(_Float16)1.f, (_Float16)1.f}, acc, false);
-    }
 };
 
 // Conflict-free 16-byte-chunk swizzle of a [rows][HD] 16-bit LDS tile (HD*2-byte rows),
@@ -202,6 +195,18 @@ template <> __device__ __forceinline__ int swz<256>(int row) {
 }
 template <int HD> __device__ __forceinline__ int lds_off(int row, int chunk) {
     return row * (HD * 2) + ((chunk ^ swz<HD>(row)) << 4);
+}
+
+// Forward K/V tile image: 8-row x 32-column subtiles of 512 B (cdna_hip_programming.md T10
+// image (a)): byte offset of 16-byte chunk `chunk` of tile row `row`.  Conflict-free for the
+// 32x32x16 row reads (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16), like the
+// plain-row XOR image, but a lane's reads then differ only by immediates except in one bit of
+// the chunk (row reads) or of the row (transposed reads): two address registers per operand
+// instead of NS (row reads) or 2*ND (transposed reads).  One LDS-DMA wave-instruction (1 KiB,
+// lane l at +16 l) fills 8 rows x 8 chunks.
+template <int HD> __device__ __forceinline__ int kv_off(int row, int chunk) {
+    return (HD * 16) * (row >> 3) + 512 * (chunk >> 2) + 64 * (row & 7) +
+           16 * ((chunk & 3) ^ ((row >> 2) & 3));
 }
 
 __device__ __forceinline__ float wave_max_halves(float x) {

@@ -192,28 +192,26 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int r = lrow0 + i * LROW_STEP;
-            *reinterpret_cast<u32x4*>(ks + lds_off<HD>(r, lc)) = ki[i];
-            *reinterpret_cast<u32x4*>(ks + VREG + lds_off<HD>(r, lc)) = vi[i];
+            *reinterpret_cast<u32x4*>(ks + kv_off<HD>(r, lc)) = ki[i];
+            *reinterpret_cast<u32x4*>(ks + VREG + kv_off<HD>(r, lc)) = vi[i];
         }
     };
 
-    // Per-lane LDS read addresses (row-independent parts of the swizzle); the
-    // buffer / half / row-block parts are compile-time offsets folded into the ds_read.
-    const char* kaddr[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) kaddr[s] = smem + lds_off<HD>(lr, 2 * s + hh);
+    // Per-lane LDS read addresses (kv_off image): the K row read of k-step s, 32-key half kt
+    // is kb[s & 1] + RB*4*kt + 512*(s >> 1) (RB = bytes of an 8-row block); the V^T transposed
+    // read (kt, sp, dt, part) is vb[part] + RB*(4 kt + 2 sp) + 512 dt.  Everything but the
+    // two base registers of each operand is an immediate offset of the ds_read.
+    constexpr int RB = HD * 16;                 // bytes of one 8-row block of the image
     const int q4 = (lane & 15) >> 2;
-    int voff[2][ND];
+    int kb[2], vb[2];
 #pragma unroll
-    for (int part = 0; part < 2; ++part) {
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-            const int r = 4 * hh + q4 + 8 * part;
-            const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            voff[part][dt] = VREG + lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
-        }
+    for (int u = 0; u < 2; ++u) {
+        kb[u] = (int)(size_t)smem + kv_off<HD>(lr, 2 * u + hh);
+        const int r = 8 * u + 4 * hh + q4;
+        const int col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        vb[u] = (int)(size_t)smem + VREG + kv_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
     }
-
+    typedef __attribute__((address_space(3))) V8 lds_v8;
     f32x16 acc_o[ND];
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) acc_o[dt] = f32x16{};
@@ -226,14 +224,14 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // K operand of S^T = K Q^T for k-step s, 32-key half `kt`, read row-wise from the LDS image
     // of buffer `buf`
     auto rd_k = [&](const int buf, const int s, const int kt) {
-        return *reinterpret_cast<const V8*>(kaddr[s] + buf * TILE + kt * 32 * HD * 2);
+        return *(const lds_v8*)(size_t)(kb[s & 1] + buf * TILE + kt * 4 * RB + 512 * (s >> 1));
     };
     // V^T operand of O^T += V^T P^T for (kt, sp, dt) through the transposing LDS read
     auto rd_v = [&](const int buf, const int i) {
         const int kt = i / (2 * ND), sp = (i / ND) & 1, dt = i % ND;
-        const char* b = smem + buf * TILE + (32 * kt + 16 * sp) * HD * 2;
-        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[0][dt]));
-        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + voff[1][dt]));
+        const int o = buf * TILE + (4 * kt + 2 * sp) * RB + 512 * dt;
+        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(vb[0] + o));
+        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(vb[1] + o));
         const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
         return __builtin_bit_cast(V8, av);
     };
@@ -269,11 +267,11 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         }
     };
     // P = exp2(S c - m c) -> T (the B operand of the PV product) for values [v0, v0 + n);
-    // the row sum accumulates the rounded P pairs (v_dot2c against ones, two chains): the
-    // normaliser is then exactly the sum of the weights the PV MFMA multiplies.  (The reference
-    // sums the fp32 P, softmax_hip.h:129-189; the two normalisers differ by at most the bf16
-    // unit roundoff 2^-9 relative, so the LSE by at most 1.95e-3.  An fp32 sum beside the
-    // QK^T MFMAs was measured: it spills at 256 VGPRs and costs 27 % of C2 throughput.)
+    // the row sum accumulates the fp32 P values, as the reference's softmax does
+    // (softmax_hip.h:129-189), so the LSE is the fp32 log-sum-exp of the scores.  (Summing the
+    // rounded bf16 pairs with v_dot2c instead costs ~14 cycles a pair beside the MFMAs and moves
+    // the LSE by up to the bf16 unit roundoff, 2^-9; the fp32 adds fit the register budget only
+    // with the two-base kv_off image.)
     typedef __attribute__((ext_vector_type(2))) float f2;
     typedef typename DT<T>::v2 T2;
     auto exp_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], const f2 m2, float (&rs)[2],
@@ -284,10 +282,12 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             const int kt = v >> 4, r = v & 15;
             f2 x = {st[kt][r], st[kt][r + 1]};
             x = __builtin_elementwise_fma(x, c2, -m2);
-            const T2 e = {(T)fast_exp2(x[0]), (T)fast_exp2(x[1])};
+            const float e0 = fast_exp2(x[0]), e1 = fast_exp2(x[1]);
+            rs[0] += e0;
+            rs[1] += e1;
+            const T2 e = {(T)e0, (T)e1};
             pb[2 * kt + (r >> 3)][r & 7] = e[0];
             pb[2 * kt + (r >> 3)][(r & 7) + 1] = e[1];
-            rs[(v >> 1) & 1] = DT<T>::sum2(e, rs[(v >> 1) & 1]);
         }
     };
     auto exp_ref = [&]() {
@@ -335,21 +335,21 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         l_run += rs[0] + rs[1];
     };
     // The pipeline's scores are X = S c - m_sc already: P = exp2(X) -> T for values [v0, v0 + n)
-    auto expx_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], const int v0, const int n) {
+    auto expx_part = [&](const f32x16 (&st)[2], V8 (&pb)[4], float& rs, const int v0, const int n) {
 #pragma unroll
         for (int v = v0; v < v0 + n; v += 2) {
             const int kt = v >> 4, r = v & 15;
-            const T2 e = {(T)fast_exp2(st[kt][r]), (T)fast_exp2(st[kt][r + 1])};
+            const float e0 = fast_exp2(st[kt][r]), e1 = fast_exp2(st[kt][r + 1]);
+            rs += e0;
+            rs += e1;
+            const T2 e = {(T)e0, (T)e1};
             pb[2 * kt + (r >> 3)][r & 7] = e[0];
             pb[2 * kt + (r >> 3)][(r & 7) + 1] = e[1];
         }
     };
     auto expx_tile = [&](const f32x16 (&st)[2], V8 (&pb)[4]) {
-        expx_part(st, pb, 0, 32);
         float rs = 0.f;
-#pragma unroll
-        for (int pi = 0; pi < 16; ++pi)
-            rs = DT<T>::sum2(T2{pb[pi >> 2][2 * (pi & 3)], pb[pi >> 2][2 * (pi & 3) + 1]}, rs);
+        expx_part(st, pb, rs, 0, 32);
         l_run += rs;
     };
     // Deferred rescale on pipeline scores: mx = this row's max of X = S c - m_sc over the new
@@ -403,16 +403,11 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // the ds_read_tr builtin as aliasing every in-flight LDS-DMA and would drain the DMA queue
     // (vmcnt(0)) before it; the asm reads are covered by explicit lgkmcnt waits instead.
     // Byte offset OFF (buffer + row block) is an immediate.
-    int vaddr[2][ND];
-#pragma unroll
-    for (int part = 0; part < 2; ++part)
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) vaddr[part][dt] = (int)(size_t)(smem) + voff[part][dt];
-    auto rd_v_asm = [&](auto OFF, const int dt) {
+    auto rd_v_asm = [&](auto OFF) {
         constexpr int off = decltype(OFF)::value;
         s16x4 t0, t1;
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t0) : "v"(vaddr[0][dt]), "i"(off));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t1) : "v"(vaddr[1][dt]), "i"(off));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t0) : "v"(vb[0]), "i"(off));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t1) : "v"(vb[1]), "i"(off));
         const s16x8 av = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
         return __builtin_bit_cast(V8, av);
     };
@@ -433,15 +428,17 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // exactly tile j+2.  The LDS image is the same swizzled image the register-staged path
     // writes: lane l of a wave-instruction lands at +16 l, so it fetches the global chunk
     // (l % CPR) ^ swz(row) of its row.
-    constexpr int RPI = 64 / CPR;                  // tile rows per DMA wave-instruction
-    constexpr int IPW = kBlockN / RPI / NW;        // DMA wave-instructions per wave per K (V) tile
-    static_assert(IPW >= 1 && IPW * RPI * NW == kBlockN, "DMA geometry");
+    constexpr int IPW = TILE / 1024 / NW;          // DMA wave-instructions per wave per K (V) tile
+    static_assert(IPW >= 1 && IPW * 1024 * NW == TILE, "DMA geometry");
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     int dma_k[IPW], dma_v[IPW];                    // per-lane byte offsets within a tile
+    constexpr int PPB = CPR / 8;                   // DMA pieces per 8-row block
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-        const int r = (wave * IPW + i) * RPI + lane / CPR;
-        const int cch = (lane % CPR) ^ swz<HD>(r);
+        // piece g = 8 rows x 8 chunks of the kv_off image: lane l lands at g KiB + 16 l
+        const int g = wave * IPW + i;
+        const int r = 8 * (g / PPB) + (lane & 31) / 4;
+        const int cch = 8 * (g % PPB) + 4 * (lane >> 5) + ((lane & 3) ^ ((r >> 2) & 3));
         const bool ok = cch * 8 < p.d;
         dma_k[i] = ok ? r * (int)p.k_row * 2 + cch * 16 : kOOB;
         dma_v[i] = ok ? r * (int)p.v_row * 2 + cch * 16 : kOOB;
@@ -501,8 +498,8 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     //
     // Scores leave phase b already scaled and shifted, X = S c - m_sc, so phase a is exp + cvt
     // only; the VALU of a tile splits evenly between the two MFMA phases (per wave and tile:
-    // a = 32 v_exp + 16 cvt beside 16 QK^T MFMAs, b = 32 fma + 16 max3 + 16 dot2c row sums beside
-    // 16 PV MFMAs), each within the MFMA gaps.  The edge mask runs after phase b on the edge tiles only.
+    // a = 32 v_exp + 32 fp32 row-sum adds + 16 cvt beside 16 QK^T MFMAs, b = 32 fma + 16 max3
+    // beside 16 PV MFMAs), each within the MFMA gaps.  The edge mask runs after phase b on the edge tiles only.
     const int lim_e = my_lr - 4 * hh;            // right edge of this lane's keys, minus its offset
     auto pipe_range = [&](const int lo, const int hm, const int hi) {
         const bool third = lo + 2 < hi;
@@ -531,6 +528,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             sn[0] = f32x16{};
             sn[1] = f32x16{};
             V8 pb[4];
+            float rs = 0.f;                       // fp32 row sum of P_j
             constexpr int EV = 32 / (2 * NS);     // exp values per QK^T MFMA
             V8 a0 = rd_k(ks, 0, 0), a1 = rd_k(ks, 0, 1);
 #pragma unroll
@@ -538,31 +536,30 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 V8 n0 = a0, n1 = a1;
                 if (s + 1 < NS) { n0 = rd_k(ks, s + 1, 0); n1 = rd_k(ks, s + 1, 1); }
                 sn[0] = DT<T>::mfma32(a0, qf[s], sn[0]);
-                expx_part(st, pb, (2 * s) * EV, EV);
+                expx_part(st, pb, rs, (2 * s) * EV, EV);
                 sn[1] = DT<T>::mfma32(a1, qf[s], sn[1]);
-                expx_part(st, pb, (2 * s + 1) * EV, EV);
+                expx_part(st, pb, rs, (2 * s + 1) * EV, EV);
                 a0 = n0;
                 a1 = n1;
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             }
             // phase b: O += V_j^T P_j on the MFMA pipe; on the VALU X_{j+1} = S_{j+1} c - m_sc
-            // (transforms and edge mask first), its row max, and the row sum of P_j; V^T read
-            // two MFMAs ahead (asm reads, explicit lgkmcnt)
+            // (transforms and edge mask first) and its row max; V^T read two MFMAs ahead (asm
+            // reads, explicit lgkmcnt)
             constexpr int MV = 32 / NPV;          // score values per PV MFMA
             auto voffs = [&](auto I) {             // immediate offset of PV operand I
                 constexpr int i = decltype(I)::value;
-                return std::integral_constant<int, vs * TILE + (32 * (i / (2 * ND)) + 16 * ((i / ND) & 1)) * HD * 2>{};
+                return std::integral_constant<int, vs * TILE + (4 * (i / (2 * ND)) + 2 * ((i / ND) & 1)) * RB + 512 * (i % ND)>{};
             };
             const float mr = exp_ref()[0];
             float mx = -INFINITY;
-            float rs = 0.f;
             V8 ring[3];
-            ring[0] = rd_v_asm(voffs(std::integral_constant<int, 0>{}), 0);
-            ring[1] = rd_v_asm(voffs(std::integral_constant<int, 1>{}), 1 % ND);
+            ring[0] = rd_v_asm(voffs(std::integral_constant<int, 0>{}));
+            ring[1] = rd_v_asm(voffs(std::integral_constant<int, 1>{}));
             static_for<NPV>([&](auto I) {
                 constexpr int i = decltype(I)::value;
                 if constexpr (i + 2 < NPV) {
-                    ring[(i + 2) % 3] = rd_v_asm(voffs(std::integral_constant<int, i + 2>{}), (i + 2) % ND);
+                    ring[(i + 2) % 3] = rd_v_asm(voffs(std::integral_constant<int, i + 2>{}));
                     lgkm_wait(std::integral_constant<int, 4>{});
                 } else if constexpr (i + 1 < NPV) {
                     lgkm_wait(std::integral_constant<int, 2>{});
@@ -579,18 +576,11 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
 #pragma unroll
                     for (int v = i * MV; v < (i + 1) * MV; ++v) mx = fmaxf(mx, sn[v >> 4][v & 15]);
                 }
-                // row sum of the rounded P_j weights: 16 pairs over the NPV MFMAs
-                constexpr int PPM = 16 / NPV;     // P pairs per PV MFMA
-#pragma unroll
-                for (int u = 0; u < PPM; ++u) {
-                    const int pi = i * PPM + u;
-                    rs = DT<T>::sum2(T2{pb[pi >> 2][2 * (pi & 3)], pb[pi >> 2][2 * (pi & 3) + 1]}, rs);
-                }
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
             });
-            // opaque uses pin the row sum and the max chain inside phase b (else they are sunk
-            // below the edge branch, out of the MFMA gaps)
-            asm volatile("" : "+v"(rs), "+v"(mx));
+            // an opaque use pins the max chain inside phase b (else it is sunk below the edge
+            // branch, out of the MFMA gaps)
+            asm volatile("" : "+v"(mx));
             l_run += rs;
             if (j + 1 >= hm) {                    // edge tile: mask, then the row max again
                 const int lim_t = lim_e - (j + 1) * kBlockN;
