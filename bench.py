@@ -9,6 +9,8 @@ Workloads (BASELINE.json configs):
   --mode varlen  C4: mha_varlen_fwd, 32 ragged sequences, total 131072 tokens, H=32 D=128 bf16.
   --mode decode  C5: paged-KV decode (fwd_kvcache), per GPU B=8 H=32 Hk=8 Sq=1, cache 32768
                  tokens, page 16, fp8 e4m3fn K/V; HBM-bound, reported in GB/s.
+  --mode fwd_fp8 the C2 shape with fp8 e4m3fn Q/K/V (per-tensor descales) on the fp8 MFMA
+                 (north_star's fp8 GEMMs; an extension, priced against the 5 PF fp8 peak).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ...] [--scaling weak|strong]
 
@@ -48,6 +50,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0       # dense fp8 (block-scaled 32x32x64) MFMA peak
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM)
 METRIC = "attention TFLOPS/GPU (fwd, fwd+bwd) at S=4096 D=128; % MI355X MFMA peak"
 
@@ -62,7 +65,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["fwd", "fwdbwd", "varlen", "decode"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "fwdbwd", "varlen", "decode", "fwd_fp8"],
+                    default="fwd")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--batch", type=int, default=0, help="default: 4 (fwd), 8 (decode)")
     ap.add_argument("--heads", type=int, default=32)
@@ -237,6 +241,40 @@ def workload_dense(a, mode, dev, rank, world):
                 cpu=lambda: cpu_baseline_dense(8, S, D, causal, a.cpu_baseline_seconds))
 
 
+def workload_fp8(a, dev, rank, world):
+    """C2 shape with fp8 e4m3fn Q/K/V (per-tensor descales), bf16 output."""
+    import xf_flash_attention_cutlass_amd as xfa
+    pa = xfa.paged_attn
+    B, S, H, D = a.batch or 4, a.seqlen or 4096, a.heads, a.headdim
+    causal = not a.no_causal
+    scale = D ** -0.5
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    sets = []
+    for _ in range(a.rotate or 2):
+        xs = []
+        for _ in range(3):
+            t = torch.randn(B, S, H, D, device=dev, generator=g)
+            s8 = float(t.abs().max()) / 448.0
+            xs.append(((t / s8).to(torch.float8_e4m3fn), s8))
+            del t
+        out = torch.empty(B, S, H, D, device=dev, dtype=torch.bfloat16)
+        sets.append((xs, out))
+    nxt = _rotating(sets)
+
+    def step():
+        (q, qs), (k, ks), (v, vs) = (x for x in nxt()[0])
+        pa.fwd_fp8(q, k, v, None, qs, ks, vs, scale, causal, -1, -1, False)
+
+    cs = "causal" if causal else "non-causal"
+    return dict(step=step, units=fwd_flops(B, H, S, S, D, causal), bound="mfma8",
+                out=lambda: sets[0][1], gather_dim=0,
+                config={"workload": f"mha_fwd fp8-e4m3 Q/K/V B={B} H={H} S={S} D={D} {cs}, "
+                                    f"bf16 out", "global_batch": B * world, "seq_len": S,
+                        "heads": H, "head_dim": D, "input_sets": a.rotate or 2,
+                        "parallelism": f"dp{world} ({a.scaling} scaling: batch shards)"},
+                cpu=lambda: cpu_baseline_dense(8, S, D, causal, a.cpu_baseline_seconds))
+
+
 def workload_varlen(a, dev, rank, world):
     import xf_flash_attention_cutlass_amd as xfa
     from xf_flash_attention_cutlass_amd import sharding
@@ -337,6 +375,8 @@ def build_workload(a, mode, dev, rank, world):
         return workload_dense(a, mode, dev, rank, world)
     if mode == "varlen":
         return workload_varlen(a, dev, rank, world)
+    if mode == "fwd_fp8":
+        return workload_fp8(a, dev, rank, world)
     return workload_decode(a, dev, rank, world)
 
 
@@ -382,9 +422,9 @@ def roofline(w, ms, mode):
     hbm = w["bound"] == "hbm"
     scale_u = 1e9 if hbm else 1e12
     achieved = w["units"] / (ms / 1e3) / scale_u
-    peak = PEAK_HBM_GBS if hbm else PEAK_BF16_TFLOPS
+    peak = PEAK_HBM_GBS if hbm else PEAK_FP8_TFLOPS if w["bound"] == "mfma8" else PEAK_BF16_TFLOPS
     tr = measured_traffic(mode)
-    roof = {"bound": w["bound"], "achieved": round(achieved, 2), "peak": peak,
+    roof = {"bound": "mfma" if w["bound"] == "mfma8" else w["bound"], "achieved": round(achieved, 2), "peak": peak,
             "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": tr["bytes"] if tr else None,
             "algorithmic_per_launch": w["units"], "kernel_ms": round(ms, 4)}
@@ -572,6 +612,7 @@ def main(argv=None):
         extras["fwd_bwd"] = sub_result(a, "fwdbwd", dev, stream)
         extras["varlen"] = sub_result(a, "varlen", dev, stream)
         extras["decode"] = sub_result(a, "decode", dev, stream)
+        extras["fwd_fp8"] = sub_result(a, "fwd_fp8", dev, stream)
     if dist:
         dist.barrier()
 
@@ -588,7 +629,9 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": a.scaling,
             "vs_baseline": None,
-            "dtype": "bf16" if not hbm else "fp8-e4m3 K/V, bf16 q/o, f32 accumulate",
+            "dtype": ("fp8-e4m3 K/V, bf16 q/o, f32 accumulate" if hbm else
+                      "fp8-e4m3 q/k/v and P, bf16 out, f32 accumulate" if a.mode == "fwd_fp8"
+                      else "bf16"),
             "data": "synthetic (torch.randn, N(0,1)), inputs resident in HBM",
             "prewarm_s": a.prewarm_s,
             "launch": "hipGraph replay of one step" if use_graph else "eager",

@@ -101,6 +101,19 @@ int fmha_set_option(const char* name, int value);
 /* Current value of a knob, or -1 (with fmha_last_error set) for an unknown name. */
 int fmha_get_option(const char* name);
 
+/* fp8 forward (extension; north_star "the two back-to-back GEMMs on ... fp8 MFMA"): q, k, v in
+ * OCP fp8 e4m3fn ([batch, seqlen, heads, 128] contiguous bytes, as fmha_fwd's layout) with
+ * per-tensor fp32 dequant scales (value = stored x scale, FA3's descale_q/k/v); both GEMMs on
+ * the gfx950 block-scaled fp8 MFMA (2x the bf16 rate), P rounded to e4m3 for the PV product.
+ * o: bf16 (out_fp16 = false) or fp16 [batch, seqlen_q, heads, 128]; softmax_lse fp32
+ * [batch, heads, seqlen_q] or NULL.  Causality / windows as fmha_fwd (causal <=> wl < 0 &&
+ * wr == 0).  head_size must be 128; no ALiBi / softcap / dropout. */
+void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q_scale,
+                  float k_scale, float v_scale, int32_t seqlen_q, int32_t seqlen_k,
+                  int32_t batch_size, int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                  float softmax_scale, int window_size_left, int window_size_right, bool out_fp16,
+                  hipStream_t stream);
+
 /* Varlen forward with the fields the reference's varlen C entry drops (paged_attn.cpp:423-433):
  * LSE out (fp32 [num_heads, total_q], unpadded as export.cpp:827; total_q = cu_seqlens_q[batch]
  * must be passed by the caller, it is only used to address the LSE), ALiBi, softcap,

@@ -19,6 +19,11 @@ Functions and the reference lines they restate:
                            vendored; semantics as used at test.py:620-635:
                            4-tuple (x_unpad, indices, cu_seqlens int32, max_seqlen))
 * `block_kvcache`       -> `_generate_block_kvcache`       test.py:1597-1621
+* `attention_fp8_pt`    -> no reference counterpart (the reference has no fp8 path): the
+                           low-precision estimate for the fp8 Q/K/V forward, i.e. attention_ref
+                           over the dequantised inputs with P rounded to e4m3 before PV, the fp8
+                           analogue of the reference's rounding of P to the input dtype.  Parity
+                           for the fp8 forward is therefore pinned only by this restatement.
 * `apply_rotary`        -> flash_attn.layers.rotary.apply_rotary_emb (third-party, not
                            vendored; semantics as used by the commented-out rotary branch of
                            test_flash_attn_kvcache, test.py:1454-1486: GPT-NeoX halves or
@@ -38,7 +43,7 @@ import torch
 __all__ = [
     "local_mask", "alibi_bias", "attention_ref", "attention_lse_ref",
     "random_padding_mask", "unpad_input", "pad_input", "block_kvcache",
-    "parity_ok", "expand_kv", "apply_rotary",
+    "parity_ok", "expand_kv", "apply_rotary", "quantize_fp8", "attention_fp8_pt",
 ]
 
 
@@ -271,3 +276,30 @@ def apply_rotary(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
         x1, x2 = xr[..., : rd // 2], xr[..., rd // 2:]
         out = torch.cat((x1 * c - x2 * sn, x1 * sn + x2 * c), dim=-1)
     return torch.cat((out, xf[..., rd:]), dim=-1).to(x.dtype)
+
+
+def quantize_fp8(x: torch.Tensor):
+    """Per-tensor OCP e4m3fn quantisation: (x8, scale) with x ~ x8.float() * scale."""
+    scale = float(x.float().abs().max()) / 448.0 or 1.0
+    return (x.float() / scale).clamp(-448, 448).to(torch.float8_e4m3fn), scale
+
+
+def attention_fp8_pt(q8, k8, v8, q_scale, k_scale, v_scale, causal=False, window_size=(-1, -1)):
+    """fp32 attention over the dequantised fp8 inputs with P = exp(s - rowmax) rounded to e4m3
+    before the PV product and the row sum taken over the unrounded P ([b, s, h, d] layout)."""
+    q, k, v = (x.float() * s for x, s in ((q8, q_scale), (k8, k_scale), (v8, v_scale)))
+    if causal:
+        window_size = (window_size[0], 0)
+    sq, sk = q.shape[1], k.shape[1]
+    k = expand_kv(k, q.shape[2])
+    v = expand_kv(v, q.shape[2])
+    scores = torch.einsum("bthd,bshd->bhts", q, k) * q.shape[-1] ** -0.5
+    if window_size[0] >= 0 or window_size[1] >= 0:
+        scores.masked_fill_(local_mask(sq, sk, window_size, device=q.device), float("-inf"))
+    m = scores.amax(-1, keepdim=True)
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    p = torch.exp(scores - m)
+    l = p.sum(-1, keepdim=True)
+    p8 = p.to(torch.float8_e4m3fn).float()
+    out = torch.einsum("bhts,bshd->bthd", p8, v) / l.permute(0, 2, 1, 3).clamp_min(1e-30)
+    return out

@@ -36,6 +36,7 @@ def _load_paged_attn():
 paged_attn = _load_paged_attn()
 
 from .interface import (  # noqa: E402
+    flash_attn_fp8_func,
     flash_attn_func,
     flash_attn_kvpacked_func,
     flash_attn_varlen_func,
@@ -46,6 +47,7 @@ from .interface import (  # noqa: E402
 __all__ = [
     "paged_attn",
     "flash_attn_func",
+    "flash_attn_fp8_func",
     "flash_attn_kvpacked_func",
     "flash_attn_varlen_func",
     "flash_attn_varlen_kvpacked_func",

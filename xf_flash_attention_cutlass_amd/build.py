@@ -70,6 +70,7 @@ def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
             src = os.path.join(CSRC, f"fmha_{kind}.hip")
             todo.append((src, os.path.join(OBJ, f"fmha_{kind}_hd{hd}_{dt}.o"), defs))
     todo.append((os.path.join(CSRC, "fmha_append.hip"), os.path.join(OBJ, "fmha_append.o"), []))
+    todo.append((os.path.join(CSRC, "fmha_fwd_fp8.hip"), os.path.join(OBJ, "fmha_fwd_fp8.o"), []))
     todo.append((os.path.join(CSRC, "fmha_api.cpp"), os.path.join(OBJ, "fmha_api.o"), []))
     if force:
         for _, out, _ in todo:

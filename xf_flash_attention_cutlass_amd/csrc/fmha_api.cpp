@@ -333,6 +333,45 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
     }
 }
 
+void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q_scale,
+                  float k_scale, float v_scale, int32_t seqlen_q, int32_t seqlen_k,
+                  int32_t batch_size, int32_t num_heads, int32_t num_heads_k, int32_t head_size,
+                  float softmax_scale, int window_size_left, int window_size_right, bool out_fp16,
+                  hipStream_t stream) {
+    try {
+        clear_error();
+        if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(head_size == 128, "the fp8 forward supports head_size 128 (got %d)", head_size);
+        REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
+        REQUIRE(q_scale > 0.f && k_scale > 0.f && v_scale > 0.f, "fp8 descales must be positive");
+        if (!slab_ok("q", seqlen_q, (int64_t)num_heads * head_size, 1) ||
+            !slab_ok("k/v", seqlen_k, (int64_t)num_heads_k * head_size, 1) ||
+            !slab_ok("o", seqlen_q, (int64_t)num_heads * head_size, 2)) return;
+        FwdParams p{};
+        p.q = q; p.k = k; p.v = v; p.o = o;
+        p.lse = (float*)softmax_lse;
+        // element strides; fp8 elements are bytes, so q/k/v strides are byte strides too
+        dense_strides(p, seqlen_q, seqlen_k, num_heads, num_heads_k, head_size);
+        p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
+        p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
+        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.wl = window_size_left; p.wr = window_size_right;
+        set_scales(p, softmax_scale, 0.f);
+        p.q_scale = q_scale; p.k_scale = k_scale; p.v_scale = v_scale;
+        Options& op = options();
+        p.device = current_device();
+        p.num_cus = num_cus(p.device);
+        p.persist_per_cu = op.fwd_persistent.load();
+        p.order = op.fwd_order.load();
+        p.max_slack = (float)op.fwd_slack.load();
+        p.num_splits = 1;
+        g_last_splits = 1;
+        hip_ok(launch_fwd_fp8(p, out_fp16, stream), "fp8 forward launch");
+    } catch (...) {
+        fail(9, "internal error in fmha_fwd_fp8");
+    }
+}
+
 void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         void* cu_seqlens_q, void* cu_seqlens_k, void* seqused_k,
                         void* block_table, int32_t block_table_stride, int32_t page_block_size,

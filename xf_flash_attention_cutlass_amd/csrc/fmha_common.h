@@ -96,7 +96,8 @@ struct FwdParams {
     float alibi_mul;           // 1 / scale_softmax (bias in working units)
     int num_splits;
     int kv_fp8;                // 1: K/V stored as fp8 e4m3fn
-    float k_scale, v_scale;
+    float k_scale, v_scale;    // fp8 K/V dequant scales (stored value x scale)
+    float q_scale;             // fp8 Q dequant scale (fp8 Q/K/V forward)
     int prio_hi;               // 1: waves NW/2.. run at s_setprio 1 (static, guide T5)
     int persistent;            // 1: persistent grid walking (row block, b*hk) items
     int n_mblocks;             // row blocks per (b, kv head) (persistent mode)

@@ -1,0 +1,41 @@
+// fmha_fwd_fp8.hip — launches of the fp8 (e4m3fn) Q/K/V forward (fmha_fwd_fp8_kernel.h), D = 128,
+// bf16 or fp16 output; persistent XCD-paired grid as the bf16 forward.
+#include "fmha_fwd_fp8_kernel.h"
+#include "fmha_launch.h"
+
+namespace xfa {
+
+template <typename T>
+static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
+    constexpr int NW = 8;
+    const bool mask = p.wl >= 0 || p.wr >= 0;
+    const int rows = p.seqlen_q * p.group;
+    const int n_mb = (rows + NW * 32 - 1) / (NW * 32);
+    dim3 grid(p.b * p.hk, n_mb, 1);
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    if (p.persist_per_cu > 0) {
+        const int items = p.b * p.hk * n_mb;
+        const int slots = p.num_cus * p.persist_per_cu;
+        if (items > slots) {
+            pp.persistent = (p.order == 1 && slots % 8 == 0) ? 2 : 1;
+            grid = dim3(slots, 1, 1);
+        }
+    }
+    const size_t smem = 4 * (size_t)kFp8Tile;     // K and V, two buffers each
+    void (*kern)(const FwdParams) = mask ? fmha_fwd_fp8_kernel<T, NW, true> : fmha_fwd_fp8_kernel<T, NW, false>;
+    static std::atomic<unsigned long long> attr_done{0};
+    if (first_on_device(attr_done, p.device)) {
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
+    return hipGetLastError();
+}
+
+hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st) {
+    return out_fp16 ? launch_fp8_t<_Float16>(p, st) : launch_fp8_t<__bf16>(p, st);
+}
+
+}  // namespace xfa

@@ -45,6 +45,9 @@ hipError_t launch_bwd_hd128_f16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd256_bf16(const BwdParams& p, hipStream_t st);
 hipError_t launch_bwd_hd256_f16(const BwdParams& p, hipStream_t st);
 
+// fp8 (e4m3fn) Q/K/V forward, D = 128 (fmha_fwd_fp8.hip): bf16 or fp16 output.
+hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st);
+
 // KV-cache append (+ rotary) pass, fmha_append.hip
 struct AppendParams {
     const void* q; void* q_out;

@@ -586,6 +586,47 @@ mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& v
     return {out, lse};
 }
 
+// fp8 e4m3fn Q/K/V forward (extension): q [b, sq, h, 128], k/v [b, sk, hk, 128] as
+// float8_e4m3fn (or uint8 bytes) with per-tensor descales; returns {out (out_dtype), lse}.
+std::vector<at::Tensor>
+mha_fwd_fp8(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+            c10::optional<at::Tensor>& out_, const float q_scale, const float k_scale,
+            const float v_scale, const float softmax_scale, bool is_causal, int window_size_left,
+            int window_size_right, const bool out_fp16) {
+    TORCH_CHECK(q.element_size() == 1 && k.element_size() == 1 && v.element_size() == 1,
+                "fp8 forward: q, k and v must be float8_e4m3fn (or uint8 bytes)");
+    CHECK_DEVICE(q); CHECK_DEVICE(k); CHECK_DEVICE(v);
+    CHECK_CONTIGUOUS(q); CHECK_CONTIGUOUS(k); CHECK_CONTIGUOUS(v);
+    TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be [b, s, h, d]");
+    const int batch_size = q.size(0), seqlen_q = q.size(1), num_heads = q.size(2), d = q.size(3);
+    const int seqlen_k = k.size(1), num_heads_k = k.size(2);
+    TORCH_CHECK(d == 128, "fp8 forward supports head_size 128");
+    CHECK_SHAPE(k, batch_size, seqlen_k, num_heads_k, d);
+    CHECK_SHAPE(v, batch_size, seqlen_k, num_heads_k, d);
+    TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
+    if (seqlen_q == 1) is_causal = false;
+    if (is_causal) window_size_right = 0;
+    if (window_size_left >= seqlen_k) window_size_left = -1;
+    if (window_size_right >= seqlen_k) window_size_right = -1;
+    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const auto odt = out_fp16 ? torch::kFloat16 : torch::kBFloat16;
+    at::Tensor out;
+    if (out_.has_value()) {
+        out = out_.value();
+        TORCH_CHECK(out.dtype() == odt, "out has the wrong dtype");
+        CHECK_DEVICE(out); CHECK_CONTIGUOUS(out);
+        CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, d);
+    } else {
+        out = torch::empty({batch_size, seqlen_q, num_heads, d}, q.options().dtype(odt));
+    }
+    auto lse = torch::empty({batch_size, num_heads, seqlen_q}, q.options().dtype(at::kFloat));
+    fmha_fwd_fp8(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), q_scale,
+                 k_scale, v_scale, seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, d,
+                 softmax_scale, window_size_left, window_size_right, out_fp16, cur_stream());
+    raise_if_failed("fwd_fp8");
+    return {out, lse};
+}
+
 PYBIND11_MODULE(paged_attn, m) {
     m.doc() = "FlashAttention for MI355X (gfx950): hand-written HIP kernels behind the paged_attn C ABI";
     m.def("fwd", &mha_fwd, "Forward pass");
@@ -594,5 +635,6 @@ PYBIND11_MODULE(paged_attn, m) {
     m.def("bwd", &mha_bwd, "Backward pass");
     m.def("varlen_bwd", &mha_varlen_bwd, "Backward pass (variable length)");
     m.def("fwd_kvcache_fp8", &mha_fwd_kvcache_fp8, "Paged decode over an fp8 e4m3fn K/V cache");
+    m.def("fwd_fp8", &mha_fwd_fp8, "Forward pass over fp8 e4m3fn q/k/v (fp8 MFMA)");
     m.def("version", []() { return std::string(fmha_version()); });
 }

@@ -44,14 +44,43 @@ class _FlashAttnFunc(torch.autograd.Function):
 
 def flash_attn_func(q, k, v, dropout_p=0.0, causal=False, window_size=(-1, -1), softcap=0.0,
                     alibi_slopes=None, deterministic=False, return_attn_probs=False, *,
-                    softmax_scale=None):
-    """q [b, sq, h, d], k/v [b, sk, hk, d] -> out [b, sq, h, d] (test.py:41-72)."""
+                    softmax_scale=None, q_descale=None, k_descale=None, v_descale=None,
+                    out_dtype=torch.bfloat16):
+    """q [b, sq, h, d], k/v [b, sk, hk, d] -> out [b, sq, h, d] (test.py:41-72).
+
+    Extension: float8_e4m3fn q/k/v (with per-tensor descales, value = stored x descale) run the
+    fp8-MFMA forward (forward only, d = 128, no ALiBi / softcap / dropout); out is `out_dtype`."""
     if softmax_scale is None:
         softmax_scale = q.shape[-1] ** (-0.5)
+    if q.dtype == torch.float8_e4m3fn:
+        out, lse = flash_attn_fp8_func(q, k, v, q_descale, k_descale, v_descale, softmax_scale,
+                                       causal, window_size, out_dtype, return_lse=True)
+        return out if not return_attn_probs else (out, lse, None)
     out, lse, s_dmask = _FlashAttnFunc.apply(q, k, v, dropout_p, softmax_scale, causal,
                                              tuple(int(w) for w in window_size), softcap,
                                              alibi_slopes, deterministic, return_attn_probs)
     return out if not return_attn_probs else (out, lse, s_dmask)
+
+
+def flash_attn_fp8_func(q, k, v, q_descale=None, k_descale=None, v_descale=None,
+                        softmax_scale=None, causal=False, window_size=(-1, -1),
+                        out_dtype=torch.bfloat16, return_lse=False):
+    """fp8 e4m3fn q [b, sq, h, 128], k/v [b, sk, hk, 128] with per-tensor descales (floats or
+    one-element tensors; None = 1.0): both GEMMs on the gfx950 fp8 MFMA.  Forward only."""
+    if q.requires_grad or k.requires_grad or v.requires_grad:
+        raise NotImplementedError("the fp8 forward has no backward")
+    if out_dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("out_dtype must be bfloat16 or float16")
+    if softmax_scale is None:
+        softmax_scale = q.shape[-1] ** (-0.5)
+
+    def _f(x):
+        return 1.0 if x is None else float(x)
+    q, k, v = (_maybe_contiguous(x) for x in (q, k, v))
+    out, lse = paged_attn.fwd_fp8(q, k, v, None, _f(q_descale), _f(k_descale), _f(v_descale),
+                                  softmax_scale, causal, int(window_size[0]), int(window_size[1]),
+                                  out_dtype == torch.float16)
+    return (out, lse) if return_lse else out
 
 
 def flash_attn_kvpacked_func(q, kv, dropout_p=0.0, softmax_scale=None, causal=False,
