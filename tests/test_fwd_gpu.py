@@ -666,3 +666,81 @@ def test_d256_backward_over_256_rejected(xfa):
     q = torch.randn(1, 64, 2, 264, dtype=torch.bfloat16, device=DEV)
     with pytest.raises(RuntimeError, match="at most 256"):
         xfa.flash_attn_func(q, q, q, causal=True)
+
+
+def test_varlen_reference_signature_capi(xfa):
+    """fmha_varlen_fwd with the reference's own signature (csrc/paged_attn.h:33-53,
+    paged_attn.cpp:385-440; causality from the windows only, is_causal ignored) through ctypes:
+    bitwise equal to the pybind varlen op and within the oracle rule per sequence."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(21)
+    h, hk, d = 6, 2, 128
+    lq, lk = [1, 300, 77, 513], [147, 300, 600, 513]
+    cu_q = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(sum(lq), h, d).bfloat16()
+    k = torch.randn(sum(lk), hk, d).bfloat16()
+    v = torch.randn(sum(lk), hk, d).bfloat16()
+    qd, kd, vd, cqd, ckd = (x.to(DEV) for x in (q, k, v, cu_q, cu_k))
+    for wl, wr, causal in ((-1, 0, True), (-1, -1, False), (64, 8, False)):
+        ref_out = xfa.flash_attn_varlen_func(qd, kd, vd, cqd, ckd, max(lq), max(lk),
+                                             causal=causal, window_size=(wl, wr) if not causal else (-1, -1))
+        o = torch.empty_like(qd)
+        L.fmha_varlen_fwd(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), o.data_ptr(),
+                          cqd.data_ptr(), ckd.data_ptr(), max(lq), max(lk), len(lq), h, hk, d,
+                          capi.stream_handle(), d ** -0.5, not causal, False, wl, wr)
+        capi.check()
+        torch.cuda.synchronize()
+        assert torch.equal(o, ref_out), (wl, wr)
+        for i in range(len(lq)):
+            a, b = int(cu_q[i]), int(cu_q[i + 1])
+            c_, e = int(cu_k[i]), int(cu_k[i + 1])
+            w = oracle_window((wl, wr), e - c_)
+            r, _ = orc.attention_ref(q[a:b][None], k[c_:e][None], v[c_:e][None], window_size=w)
+            pt, _ = orc.attention_ref(q[a:b][None], k[c_:e][None], v[c_:e][None], window_size=w,
+                                      upcast=False, reorder_ops=True)
+            _assert_parity(o[a:b][None], r, pt, what=f"ref-sig varlen seq{i} w({wl},{wr})")
+
+
+def test_page_kvcache_reference_signature_capi(xfa):
+    """fmha_page_kvcache_fwd with the reference's own signature (csrc/paged_attn.h:55-84,
+    paged_attn.cpp:442-568): block-table row stride = max_cache_seq_k / page, seqlen_k = the
+    longest cache, cache_seqlens non-cumulative; k/v/rotary/cache_batch_idx ignored as the
+    reference does.  With seqlen_k = the table's capacity (what the pybind op passes,
+    export.cpp:1703) it is bitwise equal to the pybind kvcache op (the split heuristic sees the
+    same length); within the kvcache rule."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(22)
+    b, h, hk, d, page, sk = 3, 8, 2, 128, 16, 1000
+    kc, vc, table, kp, vp, _ = orc.block_kvcache(sk, page, b, hk, d, dtype=torch.bfloat16)
+    max_cache = table.shape[1] * page
+    for sq in (1, 4):
+        q = torch.randn(b, sq, h, d).bfloat16()
+        seqlens = torch.tensor([1000, 517, 33], dtype=torch.int32)
+        qd, kpd, vpd, td, sd = (x.to(DEV) for x in (q, kp, vp, table, seqlens))
+        for causal, splits in ((False, 0), (True, 3)):
+            ref_out = xfa.flash_attn_with_kvcache(qd, kpd, vpd, cache_seqlens=sd, block_table=td,
+                                                  causal=causal, num_splits=splits)
+            o = torch.empty_like(qd)
+            L.fmha_page_kvcache_fwd(qd.data_ptr(), kpd.data_ptr(), vpd.data_ptr(), None, None,
+                                    o.data_ptr(), td.data_ptr(), sd.data_ptr(), max_cache, sq,
+                                    max_cache, b, h, hk, d, page, capi.stream_handle(), d ** -0.5,
+                                    -1, 0 if (causal and sq > 1) else -1, splits, None, None,
+                                    None, causal, False, False)
+            capi.check()
+            torch.cuda.synchronize()
+            assert torch.equal(o, ref_out), (sq, causal, splits)
+            kpm = torch.arange(sk).view(1, -1) < seqlens.view(-1, 1)
+            r, _ = orc.attention_ref(q, kc, vc, None, kpm, causal=causal and sq > 1)
+            pt, _ = orc.attention_ref(q, kc, vc, None, kpm, causal=causal and sq > 1, upcast=False,
+                                      reorder_ops=True)
+            _assert_parity(o, r, pt, mult=3.0, atol=1e-5, what=f"ref-sig kvcache sq{sq} c{causal}")
+    # a page size that does not divide the table stride argument is the caller's contract;
+    # a non-positive page size is rejected loudly
+    L.fmha_page_kvcache_fwd(qd.data_ptr(), kpd.data_ptr(), vpd.data_ptr(), None, None,
+                            o.data_ptr(), td.data_ptr(), sd.data_ptr(), max_cache, 4, sk, b, h,
+                            hk, d, 0, capi.stream_handle(), d ** -0.5, -1, -1, 0, None, None,
+                            None, False, False, False)
+    assert L.fmha_last_status() != 0
