@@ -50,8 +50,15 @@ def test_bwd_golden(xfa, name):
     dq, dk, dv = _run(xfa, t["q"], t["k"], t["v"], t["dout"], causal=m["causal"],
                       window_size=tuple(m["window"]), softcap=m["softcap"], alibi_slopes=slopes)
     torch.cuda.synchronize()
-    for nm, got in (("dq", dq), ("dk", dk), ("dv", dv)):
-        _grad_check(f"{name}:{nm}", got, t[nm + "_ref"], t[nm + "_pt"])
+    # reference gradients from the fixture; the low-precision twin's recomputed with the
+    # (bit-pinned) oracle restatement
+    bias = None
+    if m["alibi"]:
+        bias = orc.alibi_bias(t["alibi_slopes"], m["sq"], m["sk"], causal=m["causal"])
+    _, pt = _oracle_grads(t["q"], t["k"], t["v"], t["dout"], causal=m["causal"],
+                          window_size=tuple(m["window"]), softcap=m["softcap"], attn_bias=bias)
+    for nm, got, p in zip(("dq", "dk", "dv"), (dq, dk, dv), pt):
+        _grad_check(f"{name}:{nm}", got, t[nm + "_ref"], p)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
