@@ -23,7 +23,7 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
             grid = dim3(slots, 1, 1);
         }
     }
-    const size_t smem = 4 * (size_t)kFp8Tile;     // K and V, two buffers each
+    const size_t smem = 8 * (size_t)kFp8Tile;     // K and V, four buffers each
     void (*kern)(const FwdParams) = mask ? fmha_fwd_fp8_kernel<T, NW, true> : fmha_fwd_fp8_kernel<T, NW, false>;
     static std::atomic<unsigned long long> attr_done{0};
     if (first_on_device(attr_done, p.device)) {

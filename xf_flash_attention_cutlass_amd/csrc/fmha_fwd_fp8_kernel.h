@@ -56,7 +56,8 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
     constexpr int TILE = kFp8Tile;
     constexpr int IPW = TILE / 1024 / NW;    // DMA wave-instructions per wave per K (V) tile
     static_assert(IPW >= 1 && IPW * 1024 * NW == TILE, "DMA geometry");
-    constexpr int VREG = 2 * TILE;           // LDS: K tiles of buffers 0, 1, then V tiles
+    constexpr int NBUF = 4;                  // pipeline ring (the masked loop uses buffers 0, 1)
+    constexpr int VREG = NBUF * TILE;        // LDS: K tiles of buffers 0..3, then V tiles
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -137,8 +138,12 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
             __builtin_amdgcn_raw_ptr_buffer_load_lds(vrs, (lds_void*)(smem + VREG + buf * TILE + g * 1024), 16, dma_v[i], vso, 0, 0);
         }
     };
-    auto publish = [&]() {               // every DMA of this wave landed, then the workgroup's
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+    // counted vmcnt (the DMA writes are invisible to the compiler's waitcnt tracking): all of
+    // this wave's DMA landed, or all but the youngest tile's; then the workgroup barrier
+    constexpr int NDMA = 2 * IPW;            // vmem instructions per tile per wave
+    auto publish = [&](const bool one_in_flight = false) {
+        if (one_in_flight) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NDMA));
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -179,7 +184,7 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
     f32x16 acc_o[ND];
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) acc_o[dt] = f32x16{};
-    float m_sc = -INFINITY;                 // running max in scaled (log2) units
+    float m_sc = -INFINITY;                 // running max in scaled (log2) units (deferred)
     float l_run = 0.f;
 
     auto tile = [&](const int buf, const int nb) {
@@ -250,18 +255,232 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
         for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma_fp8(rd_v(buf, dt), pb, acc_o[dt]);
     };
 
-    if (nb_lo < nb_hi) {
-        dma_tile(nb_lo, 0);
+    // ---- tiles crossing a left window edge (and short ranges): one tile in flight, mask per wave
+    auto simple_range = [&](const int lo, const int hi) {
+        if (lo >= hi) return;
+        dma_tile(lo, 0);
         publish();                       // also retires the Q loads
         int buf = 0;
-        for (int nb = nb_lo; nb < nb_hi; ++nb) {
-            if (nb + 1 < nb_hi) dma_tile(nb + 1, buf ^ 1);
+        for (int nb = lo; nb < hi; ++nb) {
+            if (nb + 1 < hi) dma_tile(nb + 1, buf ^ 1);
             const int n0 = nb * kBlockN;
             if (wave_ok && n0 < w_lr_max && n0 + kBlockN > w_ll_min) tile(buf, nb);
             publish();
             buf ^= 1;
         }
+    };
+
+    // ---- tiles every row of the workgroup sees from their left edge on: the two-stage
+    // software pipeline of fmha_fwd_kernel.h.  Step j: QK^T of tile j+1 on the MFMA pipe beside
+    // exp / fp32 row sums / e4m3 cvt / regroup of P_j on the VALU, then PV of tile j beside
+    // X_{j+1} = S_{j+1} c - m and its row max.  K/V stream by LDS-DMA three tiles ahead through
+    // 4 buffers; one barrier per tile behind a counted vmcnt.  Tiles [hm, hi) cross the right
+    // edge (causal diagonal / ragged end) and are masked in registers on the way through.
+    typedef __attribute__((ext_vector_type(4))) int i32x4;
+    auto rd_v_asm = [&](auto OFF, const int dt) {     // V^T operand (dt), immediate buffer offset
+        constexpr int off = decltype(OFF)::value;
+        i32x2 t0, t1, t2, t3;
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(t0) : "v"(vaddr[dt]), "i"(off));
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(t1) : "v"(vaddr[dt]), "i"(off + 1024));
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(t2) : "v"(vaddr[dt]), "i"(off + 2048));
+        asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(t3) : "v"(vaddr[dt]), "i"(off + 3072));
+        return i32x8{t0[0], t0[1], t1[0], t1[1], t2[0], t2[1], t3[0], t3[1]};
+    };
+    auto lgkm_wait = [&](auto N) {
+        constexpr int n = decltype(N)::value;
+        __builtin_amdgcn_s_waitcnt(0xC07F | (n << 8));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const int lim_e = my_lr - 4 * hh;
+    auto pipe_range = [&](const int lo, const int hm, const int hi) {
+        const bool third = lo + 2 < hi;
+        dma_tile(lo, 0);
+        dma_tile(lo + 1, 1);
+        if (third) dma_tile(lo + 2, 2);
+        publish(third);
+        f32x16 sa[2], sb[2];
+        {   // first tile: S, mask, max, X
+            sa[0] = f32x16{};
+            sa[1] = f32x16{};
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) sa[kt] = mfma_fp8(rd_k(0, kt, s), qf[s], sa[kt]);
+            if (lo >= hm) {
+#pragma unroll
+                for (int v = 0; v < 32; ++v) {
+                    const int off = 32 * (v >> 4) + ((v & 15) & 3) + 8 * ((v & 15) >> 2);
+                    if (off >= lim_e - lo * kBlockN) sa[v >> 4][v & 15] = -INFINITY;
+                }
+            }
+            float mx = sa[0][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sa[0][r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[1][r]);
+            mx = wave_max_halves(mx);
+            const float m_new = fmaxf(m_sc, mx * c);
+            if (__any(m_new > m_sc + p.max_slack)) {
+                const float alpha = m_new == -INFINITY ? 1.f : fast_exp2(m_sc - m_new);
+                l_run *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+                m_sc = m_new;
+            }
+            const float mr = m_sc == -INFINITY ? 0.f : m_sc;
+#pragma unroll
+            for (int v = 0; v < 32; ++v) sa[v >> 4][v & 15] = __builtin_fmaf(sa[v >> 4][v & 15], c, -mr);
+        }
+        const int nsteps = hi - lo - 1;
+        auto step = [&](auto KB, auto VB, auto WB, const int j, f32x16 (&st)[2], f32x16 (&sn)[2]) {
+            constexpr int ks = decltype(KB)::value, vs = decltype(VB)::value, wb = decltype(WB)::value;
+            const bool issue = j + 3 < hi;
+            if (issue) dma_tile(j + 3, wb);
+            __builtin_amdgcn_sched_barrier(0);
+            // phase a: S_{j+1} (4 MFMAs) beside P_j = e4m3(exp2(X_j)), 8 values per MFMA
+            sn[0] = f32x16{};
+            sn[1] = f32x16{};
+            int pw[2][4];
+            float rs0 = 0.f, rs1 = 0.f;
+            i32x8 ka = rd_k(ks, 0, 0);
+            static_for<4>([&](auto M) {
+                constexpr int m = decltype(M)::value;    // MFMA m: key half m >> 1, d half m & 1
+                i32x8 kn = ka;
+                if constexpr (m + 1 < 4) kn = rd_k(ks, (m + 1) >> 1, (m + 1) & 1);
+                sn[m >> 1] = mfma_fp8(ka, qf[m & 1], sn[m >> 1]);
+                // exp values of dwords (kt = m >> 1, d = 2 (m & 1), 2 (m & 1) + 1)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int kt = m >> 1, d = 2 * (m & 1) + u;
+                    const float e0 = fast_exp2(st[kt][4 * d]), e1 = fast_exp2(st[kt][4 * d + 1]);
+                    const float e2 = fast_exp2(st[kt][4 * d + 2]), e3 = fast_exp2(st[kt][4 * d + 3]);
+                    rs0 += e0 + e1;
+                    rs1 += e2 + e3;
+                    const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
+                    pw[kt][d] = __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
+                }
+                ka = kn;
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            i32x8 pb;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const auto r = __builtin_amdgcn_permlane32_swap((unsigned)pw[0][d], (unsigned)pw[1][d], false, false);
+                pb[2 * d] = (int)r[0];
+                pb[2 * d + 1] = (int)r[1];
+            }
+            // phase b: O += V_j^T P_j (4 MFMAs, V^T read one MFMA ahead) beside
+            // X_{j+1} = S_{j+1} c - m and its row max (8 values per MFMA)
+            const float mr = m_sc == -INFINITY ? 0.f : m_sc;
+            float mx = -INFINITY;
+            i32x8 va = rd_v_asm(std::integral_constant<int, vs * TILE>{}, 0);
+            static_for<ND>([&](auto D) {
+                constexpr int dt = decltype(D)::value;
+                i32x8 vn = va;
+                if constexpr (dt + 1 < ND) {
+                    vn = rd_v_asm(std::integral_constant<int, vs * TILE>{}, dt + 1);
+                    lgkm_wait(std::integral_constant<int, 4>{});
+                } else {
+                    lgkm_wait(std::integral_constant<int, 0>{});
+                }
+                acc_o[dt] = mfma_fp8(va, pb, acc_o[dt]);
+#pragma unroll
+                for (int v = 8 * dt; v < 8 * dt + 8; ++v)
+                    sn[v >> 4][v & 15] = __builtin_fmaf(sn[v >> 4][v & 15], c, -mr);
+#pragma unroll
+                for (int v = 8 * dt; v < 8 * dt + 8; v += 2)
+                    mx = fmaxf(fmaxf(mx, sn[v >> 4][v & 15]), sn[(v + 1) >> 4][(v + 1) & 15]);
+                va = vn;
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            asm volatile("" : "+v"(mx));
+            l_run += rs0 + rs1;
+            if (j + 1 >= hm) {               // edge tile: mask, then the row max again
+                const int lim_t = lim_e - (j + 1) * kBlockN;
+                float mm = -INFINITY;
+#pragma unroll
+                for (int v = 0; v < 32; ++v) {
+                    const int off = 32 * (v >> 4) + ((v & 15) & 3) + 8 * ((v & 15) >> 2);
+                    if (off >= lim_t) sn[v >> 4][v & 15] = -INFINITY;
+                    mm = fmaxf(mm, sn[v >> 4][v & 15]);
+                }
+                mx = mm;
+            }
+            // deferred rescale on the shifted scores (fmha_fwd_kernel.h rescale_x)
+            mx = wave_max_halves(mx);
+            const bool fresh = m_sc == -INFINITY;
+            if (__any(mx > p.max_slack || (fresh && mx != -INFINITY))) {
+                asm volatile("; rescale_x");
+                const float delta = fresh ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
+                const float alpha = fresh ? 1.f : fast_exp2(-delta);
+                l_run *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+#pragma unroll
+                for (int v = 0; v < 32; ++v) sn[v >> 4][v & 15] -= delta;
+                m_sc = fresh ? (mx == -INFINITY ? -INFINITY : mx) : m_sc + delta;
+            }
+            publish(issue);
+        };
+        typedef std::integral_constant<int, 0> I0;
+        typedef std::integral_constant<int, 1> I1;
+        typedef std::integral_constant<int, 2> I2;
+        typedef std::integral_constant<int, 3> I3;
+        int r = 0;
+        while (r < nsteps) {
+            step(I1{}, I0{}, I3{}, lo + r, sa, sb);
+            if (++r >= nsteps) break;
+            step(I2{}, I1{}, I0{}, lo + r, sb, sa);
+            if (++r >= nsteps) break;
+            step(I3{}, I2{}, I1{}, lo + r, sa, sb);
+            if (++r >= nsteps) break;
+            step(I0{}, I3{}, I2{}, lo + r, sb, sa);
+            ++r;
+        }
+        // drain: the last tile's softmax and PV (its X is in sb after an odd step count)
+        f32x16 (&sl)[2] = (nsteps & 1) ? sb : sa;
+        int pw[2][4];
+        float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const float e0 = fast_exp2(sl[kt][4 * d]), e1 = fast_exp2(sl[kt][4 * d + 1]);
+                const float e2 = fast_exp2(sl[kt][4 * d + 2]), e3 = fast_exp2(sl[kt][4 * d + 3]);
+                rs0 += e0 + e1;
+                rs1 += e2 + e3;
+                const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
+                pw[kt][d] = __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
+            }
+        l_run += rs0 + rs1;
+        i32x8 pb;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const auto rr = __builtin_amdgcn_permlane32_swap((unsigned)pw[0][d], (unsigned)pw[1][d], false, false);
+            pb[2 * d] = (int)rr[0];
+            pb[2 * d + 1] = (int)rr[1];
+        }
+        const int lb = nsteps & 3;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma_fp8(rd_v(lb, dt), pb, acc_o[dt]);
+        __syncthreads();
+    };
+
+    // tile ranges as fmha_fwd_kernel.h: [nb_lo, f_lo) cross the left window edge (simple loop);
+    // [f_lo, nb_hi) run through the pipeline, [f_hi, nb_hi) masked on the way
+    int f_lo = nb_hi, f_hi = nb_hi;
+    {
+        const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
+        f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
+        f_hi = max(f_lo, min(nb_hi, lr_min / kBlockN));
+        if (nb_hi - f_lo < 2) f_lo = f_hi = nb_hi;
     }
+    simple_range(nb_lo, f_lo);
+    if (f_lo < nb_hi) pipe_range(f_lo, f_hi, nb_hi);
 
     // ---- epilogue: O = v_scale * acc / l, LSE in natural units of the dequantised scores
     const float l_full = wave_sum_halves(l_run);
