@@ -65,6 +65,8 @@ template <> struct DT16<_Float16> {
     }
 };
 
+enum { kLsdPermute = 0, kLsdVec = 1, kLsdScalar = 2 };
+
 // dS^T tile [256 keys][32 q] bf16, 64-byte rows: XOR the 16-byte chunk with bit 3 of the row
 // so the two 4-row blocks one tr-read half touches (8 rows apart) use different banks.
 __device__ __forceinline__ int ds_off(int row, int col) {
@@ -182,6 +184,12 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     constexpr int BN = bwd_block_n<HD>();
     constexpr bool VR = bwd_v_in_regs<HD>();
     constexpr int kBwdKeysPerWave = BN / NW;   // keys owned by one wave
+    // how each lane gets the LSE / D of its 4-row groups: broadcast reads of a per-wave LDS
+    // slot (fewer LDS instructions than 32 ds_bpermute: +5-7% at D = 128), except in the
+    // instances where the allocator then spills (measured per instance, -Rpass-analysis)
+    constexpr int LSD = HD <= 64 ? kLsdVec
+                      : HD <= 128 ? ((!MASK && FEAT) ? kLsdPermute : kLsdVec)
+                      : (MASK ? kLsdPermute : kLsdScalar);
     constexpr int NT = NW * 64;
     constexpr int KS = kBwdKeysPerWave / 32;     // 32-key subtiles per wave
     constexpr int BQ = kBwdBlockM;
@@ -272,7 +280,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     const bool ld_ok = lcol * 8 < p.d;
     uint4 qreg[QLD], doreg[QLD];
     // LSE (lanes 0-31, pre-multiplied by log2e) and D = rowsum(dO*O) (lanes 32-63) of the
-    // tile's 32 rows: one load per lane, prefetched with Q/dO, fetched by ds_bpermute
+    // tile's 32 rows: one load per lane, prefetched with Q/dO, shared through LDS
     // The raw value is kept until the end of the iteration: converting it right after the
     // load makes the wave wait vmcnt on it, and vmcnt is in order, so that wait would also
     // retire the previous tile's dQ atomics (thousands of cycles with every CU issuing).
@@ -384,6 +392,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     const float c = p.scale_log2;
     float* const dq_base = p.dq_accum + (DET ? (int64_t)blockIdx.y * p.acc_slice : 0);
     float lsd_cur = 0.f;
+    float* const lsd_slot = reinterpret_cast<float*>(ds_lds + wave * kBwdKeysPerWave * 64);
     if (n_iter > 0) { load_q(0); }
     __syncthreads();                     // K tile visible
     if (n_iter > 0) { store_q(); lsd_cur = lsd_value(); }
@@ -394,7 +403,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         const int tt = it - g * ntiles;
         const int head = hk_i * G + g;
         const int q0 = (t_lo + tt) * BQ;
+        // this tile's LSE / D -> a private slot in this wave's own dS^T rows (nobody reads
+        // them before this wave's dS^T store; the other waves' dQ reads ended at the last
+        // barrier), read back below as broadcast float4s
         const float lsd = lsd_cur;
+        if constexpr (LSD != kLsdPermute) lsd_slot[lane] = lsd;
         if (!VR && it + 1 < n_iter) load_q(it + 1);
 
         // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
@@ -432,13 +445,25 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             const int pos0 = q0 + 8 * gq + 4 * hh;
+            // rows 8gq + 4hh + i of this tile: slot[row] holds its LSE, slot[32 + row] its D
             float lse4[4], d4[4];
+            if constexpr (LSD == kLsdVec) {
+                const f32x4 l = *reinterpret_cast<const f32x4*>(lsd_slot + 8 * gq + 4 * hh);
+                const f32x4 dd = *reinterpret_cast<const f32x4*>(lsd_slot + 32 + 8 * gq + 4 * hh);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                // row 8gq + 4hh + i of this tile: lane (row) holds its LSE, lane 32 + row its D
-                const int src = 4 * (8 * gq + 4 * hh + i);
-                lse4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(lsd)));
-                d4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(src + 128, __float_as_int(lsd)));
+                for (int i = 0; i < 4; ++i) { lse4[i] = l[i]; d4[i] = dd[i]; }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 8 * gq + 4 * hh + i;
+                    if constexpr (LSD == kLsdScalar) {
+                        lse4[i] = lsd_slot[row];
+                        d4[i] = lsd_slot[32 + row];
+                    } else {   // lane (row) holds its LSE, lane 32 + row its D
+                        lse4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * row, __float_as_int(lsd)));
+                        d4[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * row + 128, __float_as_int(lsd)));
+                    }
+                }
             }
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
