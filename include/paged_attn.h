@@ -131,7 +131,11 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
 /* Paged-KV forward that also returns LSE (fp32 [batch, num_heads, seqlen_q]) and takes ALiBi
  * and an fp8 (OCP e4m3fn) K/V cache with per-tensor dequant scales.
  * kv_dtype: 0 = same as q (fp16/bf16), 1 = fp8 e4m3fn (k_scale/v_scale multiply the stored
- * values).  num_splits <= 0 picks a split count. */
+ * values).  num_splits <= 0 picks a split count.
+ * cache_leftpad: optional int32 [batch_size] (flash-attn's leftpad_k, block_info.h; commented
+ * out in export.cpp:1627-1634): batch b attends over cache rows [cache_leftpad[b],
+ * cache_seqlens[b]), key positions counted from cache_leftpad[b].  Only for one page per
+ * sequence (max_seqlen_k <= page_block_size), as the reference: no paged KV with leftpad. */
 void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
                               void* block_table, int32_t block_table_stride, void* cache_seqlens,
                               int32_t seqlen_q, int32_t max_seqlen_k, int32_t batch_size,
@@ -139,8 +143,8 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
                               int32_t page_block_size, float softmax_scale,
                               int window_size_left, int window_size_right, float softcap,
                               void* alibi_slopes, int32_t alibi_batch_stride, int32_t num_splits,
-                              int32_t kv_dtype, float k_scale, float v_scale, bool is_fp16,
-                              hipStream_t stream);
+                              int32_t kv_dtype, float k_scale, float v_scale,
+                              void* cache_leftpad, bool is_fp16, hipStream_t stream);
 
 /* KV-cache append with optional rotary embedding: the write step of mha_fwd_kvcache with new
  * k/v (export.cpp:1585-1669, kernel flash_fwd_kernel_hip.h:817-934 / rotary_hip.h:21-152 - never

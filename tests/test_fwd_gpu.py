@@ -390,11 +390,11 @@ def test_paged_fp8_capi(xfa):
             tab.data_ptr(), tab.stride(0), seqlens.data_ptr(), 1, sk, b, h, hk, d, page,
             d ** -0.5, -1, -1, 0.0, None, 0, 1]
     st = capi.stream_handle()
-    L.fmha_page_kvcache_fwd_ex(*args, 1, 0.02, 0.03, 0, st)
+    L.fmha_page_kvcache_fwd_ex(*args, 1, 0.02, 0.03, None, 0, st)
     torch.cuda.synchronize()
     assert L.fmha_last_status() == 0, L.fmha_last_error()
     assert torch.equal(out, ref)
-    L.fmha_page_kvcache_fwd_ex(*args, 7, 1.0, 1.0, 0, st)
+    L.fmha_page_kvcache_fwd_ex(*args, 7, 1.0, 1.0, None, 0, st)
     assert L.fmha_last_status() != 0
     assert b"kv_dtype" in L.fmha_last_error()
 
@@ -469,6 +469,69 @@ def test_kvcache_append(xfa, paged, rotary_fraction, rotary_interleaved, causal,
     pt, _ = orc.attention_ref(q_ro, k_ref, v_ref, None, kpm, causal=causal, upcast=False,
                               reorder_ops=True)
     _assert_parity(out, r, pt, mult=3.0, atol=1e-5, what="kvcache append")
+
+
+@pytest.mark.parametrize("new_kv", [False, True])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("alibi", [False, True])
+@pytest.mark.parametrize("seqlen_q,seqlen_k,hk,d", [(1, 128, 2, 128), (1, 339, 6, 64),
+                                                    (3, 339, 3, 128), (64, 256, 1, 128)])
+def test_kvcache_leftpad(xfa, new_kv, causal, alibi, seqlen_q, seqlen_k, hk, d):
+    """cache_leftpad on a dense cache, the recipe of the reference's test_flash_attn_kvcache with
+    has_leftpad=True (test.py:1427-1436, parametrised off there, test.py:1333): batch b's keys
+    are cache rows [leftpad[b], cache_seqlens[b] (+ new)), positions counted from leftpad[b]
+    (oracle key_leftpad, test.py:258-261,286-289).  seqlen_q = 1 runs the decode kernel."""
+    torch.manual_seed(1)
+    dtype = torch.bfloat16
+    b, h = 2, 6
+    q = torch.randn(b, seqlen_q, h, d, dtype=dtype)
+    kc = torch.randn(b, seqlen_k, hk, d, dtype=dtype)
+    vc = torch.randn(b, seqlen_k, hk, d, dtype=dtype)
+    seqlen_new = seqlen_q if new_kv else 0
+    cache_seqlens = torch.randint(0 if new_kv else 1, seqlen_k - seqlen_new + 1, (b,),
+                                  dtype=torch.int32)
+    leftpad = torch.cat([torch.randint(0, int(c), (1,), dtype=torch.int32) if c > 0
+                         else torch.zeros(1, dtype=torch.int32) for c in cache_seqlens])
+    arange = torch.arange(seqlen_k).view(1, -1)
+    cs = cache_seqlens.view(-1, 1)
+    kpm = (arange < cs + seqlen_new) & (arange >= leftpad.view(-1, 1))
+    k_ref, v_ref = kc.clone(), vc.clone()
+    k = v = None
+    if new_kv:
+        k = torch.randn(b, seqlen_new, hk, d, dtype=dtype)
+        v = torch.randn(b, seqlen_new, hk, d, dtype=dtype)
+        upd = (cs <= arange) & (arange < cs + seqlen_new)
+        k_ref[upd] = k.reshape(-1, hk, d)
+        v_ref[upd] = v.reshape(-1, hk, d)
+    slopes = torch.rand(b, h, dtype=torch.float32) * 0.3 if alibi else None
+    bias = orc.alibi_bias(slopes, seqlen_q, seqlen_k, None, kpm, causal=causal,
+                          key_leftpad=leftpad) if alibi else None
+    kd, vd = kc.clone().to(DEV), vc.clone().to(DEV)
+    out = xfa.flash_attn_with_kvcache(
+        q.to(DEV), kd, vd, None if k is None else k.to(DEV), None if v is None else v.to(DEV),
+        cache_seqlens=cache_seqlens.to(DEV), cache_leftpad=leftpad.to(DEV), causal=causal,
+        alibi_slopes=None if slopes is None else slopes.to(DEV))
+    torch.cuda.synchronize()
+    r, _ = orc.attention_ref(q, k_ref, v_ref, None, kpm, bias, causal=causal, key_leftpad=leftpad)
+    pt, _ = orc.attention_ref(q, k_ref, v_ref, None, kpm, bias, causal=causal, upcast=False,
+                              reorder_ops=True, key_leftpad=leftpad)
+    _assert_parity(out, r, pt, mult=3.0, atol=1e-5, what="kvcache leftpad")
+
+
+def test_kvcache_leftpad_paged_rejected(xfa):
+    """As flash-attn: no paged KV with leftpad (export.cpp:1628, commented out there)."""
+    q = torch.randn(1, 1, 4, 64, dtype=torch.float16, device=DEV)
+    kc = torch.randn(4, 16, 4, 64, dtype=torch.float16, device=DEV)
+    table = torch.arange(4, dtype=torch.int32, device=DEV).view(1, 4)
+    lens = torch.tensor([40], dtype=torch.int32, device=DEV)
+    lp = torch.tensor([3], dtype=torch.int32, device=DEV)
+    with pytest.raises(NotImplementedError):
+        xfa.flash_attn_with_kvcache(q, kc, kc, cache_seqlens=lens, block_table=table,
+                                    cache_leftpad=lp)
+    with pytest.raises(RuntimeError, match="leftpad"):
+        paged_attn = xfa.interface.paged_attn
+        paged_attn.fwd_kvcache(q, kc, kc, None, None, lens, None, None, None, table, None, None,
+                               0.125, False, -1, -1, 0.0, False, 0, lp)
 
 
 def test_kvcache_cache_batch_idx(xfa):

@@ -27,8 +27,8 @@ _SIGS = {
     "fmha_varlen_fwd_ex": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,
                            i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp],
     "fmha_page_kvcache_fwd_ex": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32,
-                                 i32, f32, C.c_int, C.c_int, f32, vp, i32, i32, i32, f32, f32, b_,
-                                 vp],
+                                 i32, f32, C.c_int, C.c_int, f32, vp, i32, i32, i32, f32, f32, vp,
+                                 b_, vp],
     "fmha_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                  f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz],
     "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],

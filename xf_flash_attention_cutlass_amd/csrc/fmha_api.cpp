@@ -447,8 +447,8 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
                               int32_t page_block_size, float softmax_scale,
                               int window_size_left, int window_size_right, float softcap,
                               void* alibi_slopes, int32_t alibi_batch_stride, int32_t num_splits,
-                              int32_t kv_dtype, float k_scale, float v_scale, bool is_fp16,
-                              hipStream_t stream) {
+                              int32_t kv_dtype, float k_scale, float v_scale,
+                              void* cache_leftpad, bool is_fp16, hipStream_t stream) {
     try {
         clear_error();
         if (!check_common(q, kcache, vcache, o, batch_size, num_heads, num_heads_k, head_size)) return;
@@ -457,6 +457,10 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
         REQUIRE(seqlen_q > 0 && max_seqlen_k > 0, "seqlen_q / seqlen_k must be positive");
         REQUIRE(kv_dtype == 0 || kv_dtype == 1, "kv_dtype must be 0 (same as q) or 1 (fp8 e4m3fn)");
         REQUIRE(block_table_stride > 0, "block_table_stride must be positive");
+        // export.cpp:1627-1628 (commented out in the reference): no paged KV with leftpad
+        REQUIRE(!cache_leftpad || max_seqlen_k <= page_block_size,
+                "cache_leftpad needs a non-paged cache (one page per sequence): Paged KV and "
+                "leftpad_k are not supported at the same time");
         if (!slab_ok("q/o", seqlen_q, (int64_t)num_heads * head_size, 2) ||
             !slab_ok("kcache/vcache page", page_block_size, (int64_t)num_heads_k * head_size, kv_dtype == 1 ? 1 : 2)) return;
         FwdParams p{};
@@ -469,6 +473,7 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
         p.bt_stride = block_table_stride;
         p.page_size = page_block_size;
         p.seqused_k = (const int*)cache_seqlens;         // non-cumulative (paged_attn.cpp:518-519)
+        p.leftpad_k = (const int*)cache_leftpad;
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = seqlen_q; p.seqlen_k = max_seqlen_k;
         set_windows(window_size_left, window_size_right, max_seqlen_k);
@@ -547,7 +552,7 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
                              max_cache_seq_k / page_block_size, cache_seqlens_k_ptr, seqlen_q,
                              seqlen_k, batch_size, num_heads, num_heads_k, head_size,
                              page_block_size, softmax_scale, window_size_left, window_size_right,
-                             0.f, nullptr, 0, num_splits, 0, 1.f, 1.f, is_fp16, stream);
+                             0.f, nullptr, 0, num_splits, 0, 1.f, 1.f, nullptr, is_fp16, stream);
 }
 
 

@@ -82,6 +82,8 @@ struct FwdParams {
     const int* cu_seqlens_q;   // varlen q (cumulative) or null
     const int* cu_seqlens_k;   // varlen k (cumulative) or null
     const int* seqused_k;      // per-batch key length (kvcache cache_seqlens / seqused_k) or null
+    const int* leftpad_k;      // kvcache cache_leftpad [b] or null: keys [lp, seqused_k) of the
+                               // cache are the sequence (key i = cache row lp + i)
     const int* block_table;    // paged K/V or null
     int bt_stride;
     int page_size;

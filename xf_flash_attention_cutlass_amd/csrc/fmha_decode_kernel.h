@@ -104,7 +104,10 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     char* vsl = smem + wave * 2 * SLICE;         // this wave's V image; K image follows
 
     const int sq = p.seqlen_q;
-    const int sk = __builtin_amdgcn_readfirstlane(p.seqused_k ? p.seqused_k[bidx] : p.seqlen_k);
+    // cache_leftpad: the sequence is cache rows [lp, seqused_k) (paged addressing only; the
+    // host allows it for one-page-per-sequence caches, where no load group can straddle a page)
+    const int lp = __builtin_amdgcn_readfirstlane(p.leftpad_k ? p.leftpad_k[bidx] : 0);
+    const int sk = __builtin_amdgcn_readfirstlane(p.seqused_k ? p.seqused_k[bidx] : p.seqlen_k) - lp;
     const int G = p.group;
     const int rows = sq * G;
     const int diag = sk - sq;
@@ -167,11 +170,11 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     int pg_next[3] = {0, 0, 0};
     auto fetch_pages = [&](const int t, int (&pg)[3]) __attribute__((always_inline)) {
         if (!paged) return;
-        const int last = (sk - 1) / p.page_size;
-        const int pi0 = __builtin_amdgcn_readfirstlane(min((t * kDecKeys) / p.page_size, last));
+        const int last = (sk + lp - 1) / p.page_size;
+        const int pi0 = __builtin_amdgcn_readfirstlane(min((t * kDecKeys + lp) / p.page_size, last));
         pg[0] = btab[pi0];
         pg[1] = btab[min(pi0 + 1, last)];
-        pg[2] = t * kDecKeys - pi0 * p.page_size;    // may exceed the page past the last row
+        pg[2] = t * kDecKeys + lp - pi0 * p.page_size;    // may exceed the page past the last row
     };
     const uint32_t page_k = (uint32_t)(p.page_size * krow_b), page_v = (uint32_t)(p.page_size * vrow_b);
     const __amdgpu_buffer_rsrc_t kseq_rs =

@@ -67,6 +67,9 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
     if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
     if (p.seqused_k) sk = p.seqused_k[bidx];
+    // cache_leftpad (block_info.h leftpad_k): the sequence is cache rows [lp, sk)
+    const int lp = p.leftpad_k ? p.leftpad_k[bidx] : 0;
+    sk -= lp;
     const int G = p.group;
     const int rows_total = sq * G;
     const int row0 = m_block * BM;
@@ -159,7 +162,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             const int n = nb * kBlockN + lrow0 + i * LROW_STEP;
             const bool ok = lc_ok && n < sk;
             if (paged) {
-                const int nc = ok ? n : 0;
+                const int nc = (ok ? n : 0) + lp;
                 const int pi = nc / p.page_size;
                 const int pg = btab[pi];
                 const int pr = nc - pi * p.page_size;

@@ -253,7 +253,8 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
                 c10::optional<at::Tensor>& block_table_, c10::optional<at::Tensor>& alibi_slopes_,
                 c10::optional<at::Tensor>& out_, const float softmax_scale, bool is_causal,
                 int window_size_left, int window_size_right, const float softcap,
-                bool is_rotary_interleaved, int num_splits) {
+                bool is_rotary_interleaved, int num_splits,
+                c10::optional<const at::Tensor>& cache_leftpad_) {
     check_qkv_dtype(q, kcache, vcache);
     const bool append = k_.has_value();
     const bool local_or_causal = is_causal || window_size_left >= 0 || window_size_right >= 0;
@@ -333,6 +334,18 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
         CHECK_CONTIGUOUS(seqlens);
         CHECK_SHAPE(seqlens, batch_size);
     }
+    // cache_leftpad (flash-attn's leftpad_k, commented out at export.cpp:1443,1627-1634): batch b's
+    // sequence is cache rows [leftpad[b], seqlens_k[b]); non-paged caches only, as there
+    at::Tensor leftpad;
+    if (cache_leftpad_.has_value()) {
+        leftpad = cache_leftpad_.value();
+        TORCH_CHECK(!paged_KV, "We don't support Paged KV and leftpad_k running at the same time yet");
+        TORCH_CHECK(leftpad.dtype() == torch::kInt32, "leftpad_k must have dtype int32");
+        CHECK_DEVICE(leftpad);
+        CHECK_CONTIGUOUS(leftpad);
+        CHECK_SHAPE(leftpad, batch_size);
+        TORCH_CHECK(seqlens.defined(), "cache_leftpad needs seqlens_k");
+    }
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
     at::Tensor q_attn = q_padded;
@@ -392,7 +405,9 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
                              batch_size, num_heads, num_heads_k, head_size, page_block_size,
                              softmax_scale, window_size_left, window_size_right, softcap,
                              alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs,
-                             num_splits, 0, 1.f, 1.f, q.dtype() == torch::kFloat16, cur_stream());
+                             num_splits, 0, 1.f, 1.f,
+                             leftpad.defined() ? leftpad.data_ptr() : nullptr,
+                             q.dtype() == torch::kFloat16, cur_stream());
     raise_if_failed("fwd_kvcache");
     if (head_size_og % 8 != 0) out = out.index({"...", torch::indexing::Slice(torch::indexing::None, head_size_og)});
     if (out_.has_value() && !out_.value().is_same(out)) out_.value().copy_(out), out = out_.value();
@@ -581,7 +596,8 @@ mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& v
                              lse.data_ptr(), bt.data_ptr(), (int)bt.stride(0), seqlens_k.data_ptr(),
                              seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, d, page,
                              softmax_scale, window_size_left, window_size_right, 0.f, nullptr, 0,
-                             num_splits, 1, k_scale, v_scale, dt == torch::kFloat16, cur_stream());
+                             num_splits, 1, k_scale, v_scale, nullptr, dt == torch::kFloat16,
+                             cur_stream());
     raise_if_failed("fwd_kvcache_fp8");
     return {out, lse};
 }
@@ -631,7 +647,15 @@ PYBIND11_MODULE(paged_attn, m) {
     m.doc() = "FlashAttention for MI355X (gfx950): hand-written HIP kernels behind the paged_attn C ABI";
     m.def("fwd", &mha_fwd, "Forward pass");
     m.def("varlen_fwd", &mha_varlen_fwd, "Forward pass (variable length)");
-    m.def("fwd_kvcache", &mha_fwd_kvcache, "Forward pass, with KV-cache");
+    // the reference's positional signature (export.cpp:1757) plus an optional trailing
+    // cache_leftpad
+    m.def("fwd_kvcache", &mha_fwd_kvcache, "Forward pass, with KV-cache", py::arg("q"),
+          py::arg("kcache"), py::arg("vcache"), py::arg("k"), py::arg("v"), py::arg("seqlens_k"),
+          py::arg("rotary_cos"), py::arg("rotary_sin"), py::arg("cache_batch_idx"),
+          py::arg("block_table"), py::arg("alibi_slopes"), py::arg("out"),
+          py::arg("softmax_scale"), py::arg("is_causal"), py::arg("window_size_left"),
+          py::arg("window_size_right"), py::arg("softcap"), py::arg("is_rotary_interleaved"),
+          py::arg("num_splits"), py::arg("cache_leftpad") = py::none());
     m.def("bwd", &mha_bwd, "Backward pass");
     m.def("varlen_bwd", &mha_varlen_bwd, "Backward pass (variable length)");
     m.def("fwd_kvcache_fp8", &mha_fwd_kvcache_fp8, "Paged decode over an fp8 e4m3fn K/V cache");

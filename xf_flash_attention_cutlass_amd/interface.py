@@ -164,9 +164,9 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
     fp8 * k_scale / v_scale); it requires `block_table` and `cache_seqlens`."""
     assert k_cache.stride(-1) == 1, "k_cache must have contiguous last dimension"
     assert v_cache.stride(-1) == 1, "v_cache must have contiguous last dimension"
-    if cache_leftpad is not None:
-        raise NotImplementedError("cache_leftpad is not supported (the reference does not "
-                                  "pass it to its C ABI either, test.py:233)")
+    if cache_leftpad is not None and (block_table is not None or k_cache.dtype == torch.float8_e4m3fn):
+        raise NotImplementedError("cache_leftpad needs a non-paged cache (flash-attn: no Paged KV "
+                                  "and leftpad_k at the same time)")
     q, k, v = (_maybe_contiguous(x) for x in (q, k, v))
     if softmax_scale is None:
         softmax_scale = q.shape[-1] ** (-0.5)
@@ -194,5 +194,5 @@ def flash_attn_with_kvcache(q, k_cache, v_cache, k=None, v=None, rotary_cos=None
                                       rotary_sin, cache_batch_idx, block_table, alibi_slopes,
                                       None, softmax_scale, causal, int(window_size[0]),
                                       int(window_size[1]), softcap, rotary_interleaved,
-                                      num_splits)
+                                      num_splits, _maybe_contiguous(cache_leftpad))
     return (out, lse) if return_softmax_lse else out
