@@ -542,6 +542,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 expx_part(st, pb, rs, (2 * s) * EV, EV);
                 sn[1] = DT<T>::mfma32(a1, qf[s], sn[1]);
                 expx_part(st, pb, rs, (2 * s + 1) * EV, EV);
+                // pins the row-sum adds into this MFMA gap: unpinned, the compiler sinks them
+                // below phase b (rs is only read there) into a VALU-only run of 32 adds
+                // (+1.5-2 % C2, same-box A/B)
+                asm volatile("" : "+v"(rs));
                 a0 = n0;
                 a1 = n1;
                 if (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
@@ -603,23 +607,66 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         typedef std::integral_constant<int, 1> I1;
         typedef std::integral_constant<int, 2> I2;
         typedef std::integral_constant<int, 3> I3;
-        // step r (tile j = lo + r) reads K of j+1 from buffer (r+1)%4 and V of j from r%4
+        // step r (tile j = lo + r) reads K of j+1 from buffer (r+1)%4 and V of j from r%4.
+        // Causal diagonal / right window edge: a wave stops after the last tile any of its rows
+        // sees (visible keys are contiguous) — drains it, then only issues its DMA share and
+        // joins the barriers for the rest of the workgroup's steps (the same barrier count).
+        // The skipped tiles would add exact zeros, so results are bit-identical, and the
+        // wave's SIMD partner gets the whole issue port meanwhile.
+        const int t_w = __builtin_amdgcn_readfirstlane((w_lr_max + kBlockN - 1) / kBlockN - 1);
+        const int nsteps_w = wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps;
         int r = 0;
-        while (r < nsteps) {
+        while (r < nsteps_w) {
             step(I1{}, I0{}, I3{}, lo + r, sa, sb);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I2{}, I1{}, I0{}, lo + r, sb, sa);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I3{}, I2{}, I1{}, lo + r, sa, sb);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I0{}, I3{}, I2{}, lo + r, sb, sa);
             ++r;
         }
-        // drain: the last tile's softmax and PV
+        // drain: the wave's last tile's softmax and PV.  V^T through the asm reads: a wave that
+        // leaves early still has its DMA share of tile j+3 in flight, and the builtin
+        // transposing read would make the compiler drain it (vmcnt(0)) first
         V8 pb[4];
-        if (nsteps & 1) expx_tile(sb, pb);
+        if (nsteps_w & 1) expx_tile(sb, pb);
         else expx_tile(sa, pb);
-        pv(nsteps & 3, pb);
+        auto pv_asm = [&](auto VB) {
+            constexpr int vs = decltype(VB)::value;
+            auto voffs = [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                return std::integral_constant<int, vs * TILE + (4 * (i / (2 * ND)) + 2 * ((i / ND) & 1)) * RB + 512 * (i % ND)>{};
+            };
+            V8 ring[3];
+            ring[0] = rd_v_asm(voffs(std::integral_constant<int, 0>{}));
+            ring[1] = rd_v_asm(voffs(std::integral_constant<int, 1>{}));
+            static_for<NPV>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if constexpr (i + 2 < NPV) {
+                    ring[(i + 2) % 3] = rd_v_asm(voffs(std::integral_constant<int, i + 2>{}));
+                    lgkm_wait(std::integral_constant<int, 4>{});
+                } else if constexpr (i + 1 < NPV) {
+                    lgkm_wait(std::integral_constant<int, 2>{});
+                } else {
+                    lgkm_wait(std::integral_constant<int, 0>{});
+                }
+                acc_o[i % ND] = DT<T>::mfma32(ring[i % 3], pb[i / ND], acc_o[i % ND]);
+            });
+        };
+        switch (nsteps_w & 3) {
+            case 0: pv_asm(I0{}); break;
+            case 1: pv_asm(I1{}); break;
+            case 2: pv_asm(I2{}); break;
+            default: pv_asm(I3{}); break;
+        }
+        // the steps this wave skips: its DMA share and the barriers only
+        for (; r < nsteps; ++r) {
+            const int j = lo + r;
+            const bool issue = j + 3 < hi;
+            if (issue) dma_tile(j + 3, (r + 3) & 3);
+            publish(issue);
+        }
         __syncthreads();
     };
     // Key tiles: [nb_lo, f_lo) cross the left window edge (per-wave masked loop);
