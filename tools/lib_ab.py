@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd"])
+    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwd_fp8"])
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
@@ -66,7 +66,14 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
 
+    if a.mode == "fwd_fp8":
+        q8, k8, v8 = (t.to(torch.float8_e4m3fn) for t in (q, k, v))
+
     def run(lib):
+        if a.mode == "fwd_fp8":
+            lib.fmha_fwd_fp8(P(q8), P(k8), P(v8), P(o), P(lse), 1.0, 1.0, 1.0, a.s, a.s, a.b, a.h,
+                             hk, a.d, sc, -1, wr, False, stream)
+            return
         lib.fmha_fwd(P(q), P(k), P(v), P(o), None, a.s, a.s, a.b, a.h, hk, a.d, 0.0, stream, None,
                      sc, None, P(lse), -1, wr, 0.0, False, False, 0)
         if a.mode == "bwd":

@@ -361,6 +361,9 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
                     const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
                     pw[kt][d] = __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
                 }
+                // keep the row-sum adds in this MFMA gap (fmha_fwd_kernel.h: else sunk below
+                // phase b)
+                asm volatile("" : "+v"(rs0), "+v"(rs1));
                 ka = kn;
                 __builtin_amdgcn_sched_barrier(0);
             });
@@ -430,19 +433,24 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
         typedef std::integral_constant<int, 1> I1;
         typedef std::integral_constant<int, 2> I2;
         typedef std::integral_constant<int, 3> I3;
+        // per-wave early exit past the causal diagonal / right window edge, as
+        // fmha_fwd_kernel.h: a wave stops after the last tile any of its rows sees, drains it,
+        // then keeps only its DMA share and the barriers (bit-identical results)
+        const int t_w = __builtin_amdgcn_readfirstlane((w_lr_max + kBlockN - 1) / kBlockN - 1);
+        const int nsteps_w = wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps;
         int r = 0;
-        while (r < nsteps) {
+        while (r < nsteps_w) {
             step(I1{}, I0{}, I3{}, lo + r, sa, sb);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I2{}, I1{}, I0{}, lo + r, sb, sa);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I3{}, I2{}, I1{}, lo + r, sa, sb);
-            if (++r >= nsteps) break;
+            if (++r >= nsteps_w) break;
             step(I0{}, I3{}, I2{}, lo + r, sb, sa);
             ++r;
         }
-        // drain: the last tile's softmax and PV (its X is in sb after an odd step count)
-        f32x16 (&sl)[2] = (nsteps & 1) ? sb : sa;
+        // drain: the wave's last tile's softmax and PV (its X is in sb after an odd step count)
+        f32x16 (&sl)[2] = (nsteps_w & 1) ? sb : sa;
         int pw[2][4];
         float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
@@ -464,9 +472,29 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
             pb[2 * d] = (int)rr[0];
             pb[2 * d + 1] = (int)rr[1];
         }
-        const int lb = nsteps & 3;
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) acc_o[dt] = mfma_fp8(rd_v(lb, dt), pb, acc_o[dt]);
+        // V^T by the asm reads: an early-leaving wave still has DMA in flight, which the
+        // builtin transposing read would make the compiler drain first
+        auto pv_asm = [&](auto VB) {
+            constexpr int vs = decltype(VB)::value;
+            static_for<ND>([&](auto D) {
+                constexpr int dt = decltype(D)::value;
+                const i32x8 va = rd_v_asm(std::integral_constant<int, vs * TILE>{}, dt);
+                lgkm_wait(std::integral_constant<int, 0>{});
+                acc_o[dt] = mfma_fp8(va, pb, acc_o[dt]);
+            });
+        };
+        switch (nsteps_w & 3) {
+            case 0: pv_asm(I0{}); break;
+            case 1: pv_asm(I1{}); break;
+            case 2: pv_asm(I2{}); break;
+            default: pv_asm(I3{}); break;
+        }
+        for (; r < nsteps; ++r) {
+            const int j = lo + r;
+            const bool issue = j + 3 < hi;
+            if (issue) dma_tile(j + 3, (r + 3) & 3);
+            publish(issue);
+        }
         __syncthreads();
     };
 
