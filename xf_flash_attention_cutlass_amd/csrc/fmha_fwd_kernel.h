@@ -600,7 +600,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 }
                 mx = mm;
             }
-            rescale_x(wave_max_halves(mx), sn);
+            // the decision needs no row max: some lane's half-row max passes the slack iff some
+            // row's does, so the halves are combined only on the (rare) rescale path
+            if (__any(mx > p.max_slack || (m_sc == -INFINITY && mx != -INFINITY)))
+                rescale_x(wave_max_halves(mx), sn);
             publish(issue);                       // tile j+2 landed everywhere
         };
         typedef std::integral_constant<int, 0> I0;
