@@ -6,8 +6,11 @@
 // of query rows (seqlen_q * H/Hk <= 32) fits one 32-row MFMA tile.  Decode reads every K/V
 // byte exactly once, so the design goal is bytes in flight, not MFMA rate:
 //
-//  * every wave is its own split: a 4-wave workgroup owns one (batch, kv head) and 4 key
-//    ranges; no barrier, no workgroup-level LDS sharing;
+//  * every wave is its own split, no barrier, no workgroup-level LDS sharing; the waves of a
+//    workgroup are 4 (or 8) kv heads of one (batch, key range) — their rows sit side by side in
+//    every cache row, so a workgroup's loads cover contiguous 512 B (1 KiB) runs of each row
+//    (dec_hmaj; +5 % on C5 over 4 key ranges of one kv head, whose 128-byte fp8 rows are 1 KiB
+//    apart);
 //  * K and V are loaded coalesced (consecutive lanes read consecutive 16-byte chunks of a
 //    row), dequantised, and written to a wave-private 32-key LDS image (the swizzled image of
 //    fmha_common.h), from which K is read as the A operand of S^T = K Q^T and V transposed
@@ -74,8 +77,8 @@ __device__ __forceinline__ float quad_sum16(float x) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int HD, typename T, bool KV8, int MR>
-__global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const FwdParams p) {
+template <int HD, typename T, bool KV8, int MR, int NWV = kDecWaves>
+__global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParams p) {
     using V8 = typename DT<T>::v8;
     static_assert(MR == 16 || MR == 32, "MFMA rows");
     constexpr int NS = MR == 32 ? HD / 16 : HD / 32;   // k-steps of S^T = K Q^T
@@ -97,10 +100,19 @@ __global__ void __launch_bounds__(kDecWaves * 64, 2) fmha_decode_kernel(const Fw
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & (MR - 1);               // query row (MFMA column) of this lane
     const int hh = lane / MR;                     // key sub-block (0..64/MR-1) of this lane
-    const int bh = blockIdx.x;
-    const int bidx = bh / p.hk;
-    const int hk_i = bh - bidx * p.hk;
-    const int split = blockIdx.y * kDecWaves + wave;
+    // wave -> (batch, kv head, split): 4 splits of one kv head, or (dec_hmaj) 4 kv heads of one
+    // split, whose rows sit side by side in each cache row (HD * ESZ bytes apart)
+    int bidx, hk_i, split;
+    if (p.dec_hmaj) {
+        const int g4 = p.hk / NWV;
+        bidx = blockIdx.x / g4;
+        hk_i = (blockIdx.x - bidx * g4) * NWV + wave;
+        split = blockIdx.y;
+    } else {
+        bidx = blockIdx.x / p.hk;
+        hk_i = blockIdx.x - bidx * p.hk;
+        split = blockIdx.y * kDecWaves + wave;
+    }
     char* vsl = smem + wave * 2 * SLICE;         // this wave's V image; K image follows
 
     const int sq = p.seqlen_q;

@@ -40,11 +40,26 @@ static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
 
 template <int HD, typename T>
 static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
-    const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
-    dim3 grid(p.b * p.hk, p.num_splits / kDecWaves);
-    if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
-    else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
-    hipError_t e = hipGetLastError();
+    hipError_t e;
+    if (p.dec_hmaj == 2) {
+        // 8 waves = the 8 kv heads of one split: one cache row's heads are read side by side
+        constexpr int NWV = 2 * kDecWaves;
+        const size_t smem = (size_t)NWV * 2 * kDecKeys * HD * 2;
+        static std::atomic<unsigned long long> attr_done{0};
+        if (first_on_device(attr_done, p.device)) {
+            (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, true, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        }
+        const dim3 grid(p.b * p.hk / NWV, p.num_splits);
+        if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
+        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
+    } else {
+        const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
+        const dim3 grid = p.dec_hmaj ? dim3(p.b * p.hk / kDecWaves, p.num_splits) : dim3(p.b * p.hk, p.num_splits / kDecWaves);
+        if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+    }
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
 }

@@ -25,6 +25,8 @@ struct Options {
     std::atomic<int> fwd_pipe{1};        // software-pipelined loop over the unmasked key tiles
     std::atomic<int> fwd_decode{1};      // split-KV decode kernel when seqlen_q * H/Hk <= 32
     std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
+    std::atomic<int> dec_hmaj{1};        // decode workgroup: 0 = 1 kv head x 4 splits, 1 = 4 kv heads x one
+                                         // split, 2 = 8 kv heads x one split (C5 fp8: 116 / 110 / 112 us)
 };
 Options& options();
 
