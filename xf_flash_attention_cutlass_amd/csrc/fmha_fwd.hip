@@ -56,8 +56,16 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     } else {
         const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
         const dim3 grid = p.dec_hmaj ? dim3(p.b * p.hk / kDecWaves, p.num_splits) : dim3(p.b * p.hk, p.num_splits / kDecWaves);
-        if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
-        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+        if (p.dec_rx && p.kv_fp8) {
+            if (p.dec_mr == 16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16, kDecWaves, 1>), grid, dim3(kDecWaves * 64), smem, st, p);
+            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32, kDecWaves, 1>), grid, dim3(kDecWaves * 64), smem, st, p);
+        } else if (p.dec_mr == 16) {
+            if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
+            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
+        } else {
+            if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32>), grid, dim3(kDecWaves * 64), smem, st, p);
+        }
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
