@@ -229,7 +229,6 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         // head-major workgroups (4 or 8 kv heads of one split) when the kv heads divide evenly
         const int hm = o.dec_hmaj.load();
         p.dec_mr = (o.dec_mr.load() == 16 && p.seqlen_q * p.group <= 16) ? 16 : 32;
-        p.dec_rx = o.dec_rx.load();
         p.dec_hmaj = (hm == 2 && p.hk % 8 == 0) ? 2 : (hm >= 1 && p.hk % 4 == 0) ? 1 : 0;
     } else if (p.cu_seqlens_q) {
         splits = 1;  // varlen: single pass (the reference forces it too)
@@ -280,7 +279,6 @@ int fmha_set_option(const char* name, int value) {
         {"fwd_xcdq", &o.fwd_xcdq, 0, 1},         {"fwd_pipe", &o.fwd_pipe, 0, 2},
         {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
-        {"dec_rx", &o.dec_rx, 0, 1},
         {"dec_mr", &o.dec_mr, 16, 32},
     };
     for (const Knob& k : knobs) {
@@ -304,7 +302,7 @@ int fmha_get_option(const char* name) {
 #define XFA_GET(n) if (!strcmp(name, #n)) return o.n.load();
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
-    XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(dec_rx)
+    XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;

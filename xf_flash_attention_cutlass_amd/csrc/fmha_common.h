@@ -108,7 +108,6 @@ struct FwdParams {
                                // O / l rescale (deferred rescale; 0 = rescale on every rise)
     int decode;                // 1: run fmha_decode_kernel (split-KV decode)
     int dec_mr;                // decode: 16 -> the 16x16x32 tile (query rows <= 16)
-    int dec_rx;                // decode: one more fp8 tile in the load ring
     int dec_hmaj;              // decode: the 4 waves of a workgroup are 4 kv heads of one split
     int* work_ctr;             // persistent == 3: self-resetting counters [-, finished, next x 8]
     int xcd_queues;            // persistent == 3: one item queue per XCD (else queue 0 only)

@@ -77,7 +77,7 @@ __device__ __forceinline__ float quad_sum16(float x) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int HD, typename T, bool KV8, int MR, int NWV = kDecWaves, int RX = 0>
+template <int HD, typename T, bool KV8, int MR, int NWV = kDecWaves>
 __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParams p) {
     using V8 = typename DT<T>::v8;
     static_assert(MR == 16 || MR == 32, "MFMA rows");
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
     constexpr int NLD = kDecKeys / RPI;          // load instructions per lane per K (V) tile
     // tiles in flight beyond the current one (bounded by the 256-VGPR budget of two waves
     // per SIMD; the 16-row tile frees the registers for one more fp8 tile)
-    constexpr int RING = (KV8 ? (MR == 16 ? 3 : 2) : 1) + RX;
+    constexpr int RING = KV8 ? (MR == 16 ? 3 : 2) : 1;
     constexpr int SLICE = kDecKeys * HD * 2;     // LDS bytes of one wave's K (or V) image
     extern __shared__ __attribute__((aligned(16))) char smem[];
 

@@ -49,17 +49,21 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
         if (first_on_device(attr_done, p.device)) {
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, true, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, true, 16, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 16, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         }
         const dim3 grid(p.b * p.hk / NWV, p.num_splits);
-        if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
-        else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
+        if (p.dec_mr == 16) {
+            if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16, NWV>), grid, dim3(NWV * 64), smem, st, p);
+            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16, NWV>), grid, dim3(NWV * 64), smem, st, p);
+        } else {
+            if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
+            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 32, NWV>), grid, dim3(NWV * 64), smem, st, p);
+        }
     } else {
         const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
         const dim3 grid = p.dec_hmaj ? dim3(p.b * p.hk / kDecWaves, p.num_splits) : dim3(p.b * p.hk, p.num_splits / kDecWaves);
-        if (p.dec_rx && p.kv_fp8) {
-            if (p.dec_mr == 16) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16, kDecWaves, 1>), grid, dim3(kDecWaves * 64), smem, st, p);
-            else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 32, kDecWaves, 1>), grid, dim3(kDecWaves * 64), smem, st, p);
-        } else if (p.dec_mr == 16) {
+        if (p.dec_mr == 16) {
             if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
             else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
         } else {

@@ -27,7 +27,6 @@ struct Options {
     std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
     std::atomic<int> dec_mr{16};         // decode MFMA rows: 16 when the query rows fit 16 (C5: 105 vs
                                          // 110 us with dec_hmaj = 1), else 32
-    std::atomic<int> dec_rx{0};          // decode: one more fp8 tile in the load ring
     std::atomic<int> dec_hmaj{1};        // decode workgroup: 0 = 1 kv head x 4 splits, 1 = 4 kv heads x one
                                          // split, 2 = 8 kv heads x one split (C5 fp8: 116 / 110 / 112 us)
 };
