@@ -387,12 +387,14 @@ def measured_traffic(mode):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
     if not files:
         return None
-    try:
-        d = json.load(open(files[-1])).get(mode)
-        return None if d is None else {"bytes": d["hbm_bytes_per_launch"], "file":
-                                       os.path.relpath(files[-1], ROOT)}
-    except (OSError, ValueError, KeyError):
-        return None
+    for f in reversed(files):            # the newest summary that profiled this mode
+        try:
+            d = json.load(open(f)).get(mode)
+        except (OSError, ValueError):
+            continue
+        if d is not None and "hbm_bytes_per_launch" in d:
+            return {"bytes": d["hbm_bytes_per_launch"], "file": os.path.relpath(f, ROOT)}
+    return None
 
 
 def event_ms(step, steps, stream):
