@@ -87,7 +87,8 @@ int fmha_last_status(void);
  * kernel: one split per wave).  Diagnostic, for tests and tuning. */
 int fmha_last_num_splits(void);
 
-/* Library version / build identification, e.g. "xf-fmha-gfx950 1.0". */
+/* Library version / build identification, e.g. "xf-fmha-gfx950 2.0".  2.0 (round 3) changed
+ * argument lists of existing symbols (see INTEGRATION.md "ABI history"). */
 const char* fmha_version(void);
 
 /* Process-wide schedule knobs; every setting computes the same results (the parity suite runs
@@ -96,7 +97,8 @@ const char* fmha_version(void);
  * -1 for an unknown name / out-of-range value.  Knobs: fwd_waves (4 | 8 waves = 128 | 256
  * query rows per forward workgroup), fwd_prio (0/1), fwd_persistent (workgroups per CU, 0 =
  * one workgroup per item), fwd_slack (0..16), fwd_order (0/1), fwd_dyn (0..2), fwd_xcdq (0/1),
- * fwd_pipe (0..2), fwd_decode (0/1), dec_wg_per_cu (1..16). */
+ * fwd_pipe (0..2), fwd_decode (0/1), dec_wg_per_cu (1..16), dec_hmaj (0..2), dec_mr (16/32),
+ * fwd_w4 (0/1: the 4-wave D = 128 forward where eligible). */
 int fmha_set_option(const char* name, int value);
 /* Current value of a knob, or -1 (with fmha_last_error set) for an unknown name. */
 int fmha_get_option(const char* name);
@@ -108,6 +110,17 @@ int fmha_get_option(const char* name);
  * o: bf16 (out_fp16 = false) or fp16 [batch, seqlen_q, heads, 128]; softmax_lse fp32
  * [batch, heads, seqlen_q] or NULL.  Causality / windows as fmha_fwd (causal <=> wl < 0 &&
  * wr == 0).  head_size must be 128; no ALiBi / softcap / dropout. */
+/* fmha_fwd with explicit ELEMENT strides for q, k, v, o (batch, row, head; the last dimension
+ * is contiguous): head- or batch-sliced views run without a copy (the reference's C ABI assumes
+ * contiguous tensors, csrc/paged_attn.cpp:46-60).  strides[12] = {q_batch, q_row, q_head,
+ * k_batch, k_row, k_head, v_batch, v_row, v_head, o_batch, o_row, o_head}.  softmax_lse is
+ * [batch, num_heads, seqlen_q] contiguous (or NULL).  head_size must be a multiple of 8. */
+void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, void* softmax_lse,
+                      int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
+                      int32_t num_heads_k, int32_t head_size, const int64_t* strides,
+                      float softmax_scale, int window_size_left, int window_size_right,
+                      float softcap, bool is_fp16, int num_splits, hipStream_t stream);
+
 void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q_scale,
                   float k_scale, float v_scale, int32_t seqlen_q, int32_t seqlen_k,
                   int32_t batch_size, int32_t num_heads, int32_t num_heads_k, int32_t head_size,

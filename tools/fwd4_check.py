@@ -1,0 +1,157 @@
+"""A/B check of the 4-wave D = 128 forward (fwd_w4=1) against the 8-wave kernel (fwd_w4=0) and
+a torch fp32 reference: every case goes through varlen_fwd (one split, so the dense-path split
+heuristic cannot route small shapes away from the kernel under test).  Prints max |dO| vs the
+8-wave kernel and vs fp32, and on a mismatch where the error sits (row block / wave / lane
+half / head-dim column block).  --time then times C2 (dense, causal) with each kernel.
+
+  python tools/fwd4_check.py [--time] [--shapes small|all]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import xf_flash_attention_cutlass_amd as xfa  # noqa: E402
+from xf_flash_attention_cutlass_amd import capi  # noqa: E402
+
+pa = xfa.paged_attn
+
+
+def opt(name, v):
+    assert capi.lib().fmha_set_option(name.encode(), v) == 0
+
+
+def ref(q, k, v, lq, lk, causal):
+    """fp32 reference per sequence; q [tq, h, d] packed."""
+    h, hk = q.shape[1], k.shape[1]
+    outs = []
+    oq = ok = 0
+    for a, b in zip(lq, lk):
+        qq = q[oq:oq + a].float().transpose(0, 1)
+        kk = k[ok:ok + b].float().transpose(0, 1).repeat_interleave(h // hk, 0)
+        vv = v[ok:ok + b].float().transpose(0, 1).repeat_interleave(h // hk, 0)
+        s = qq @ kk.transpose(1, 2) * q.shape[-1] ** -0.5
+        if causal:
+            i = torch.arange(a, device=q.device)[:, None]
+            j = torch.arange(b, device=q.device)[None, :]
+            s = s.masked_fill(j > i + (b - a), float("-inf"))
+        p = torch.softmax(s, -1).nan_to_num(0.0)
+        outs.append((p @ vv).transpose(0, 1))
+        oq += a
+        ok += b
+    return torch.cat(outs)
+
+
+def run(q, k, v, lq, lk, causal, w4):
+    opt("fwd_w4", w4)
+    dev = q.device
+    cq = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32, device=dev)
+    ck = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32, device=dev)
+    out = torch.empty_like(q)
+    r = pa.varlen_fwd(q, k, v, out, cq, ck, None, None, None, max(lq), max(lk), 0.0,
+                      q.shape[-1] ** -0.5, False, causal, -1, 0 if causal else -1, 0.0, False, None)
+    torch.cuda.synchronize()
+    return r[0], r[5]
+
+
+def where(err, lq, G):
+    """Localise errors of [tq, h, d]: first sequence, rows as the kernel sees them (pos*G+g)."""
+    e = err[:lq[0]]                                   # [sq, h, d]
+    sq, h, d = e.shape
+    hk = h // G
+    rows = e.reshape(sq, hk, G, d).permute(1, 0, 2, 3).reshape(hk, sq * G, d)
+    rmax = rows.amax(dim=(0, 2))                      # per kernel row
+    bad = (rmax > 0.05).nonzero().flatten().tolist()
+    cmax = rows.amax(dim=(0, 1))
+    badc = (cmax > 0.05).nonzero().flatten().tolist()
+    print(f"    bad kernel rows ({len(bad)}): {bad[:12]}{'...' if len(bad) > 12 else ''}")
+    print(f"    by row%64 lane-row: {sorted(set(r % 32 for r in bad))[:16]}  "
+          f"wave {sorted(set((r % 256) // 64 for r in bad))}  rb {sorted(set((r % 64) // 32 for r in bad))}")
+    print(f"    bad d columns ({len(badc)}): {badc[:16]}{'...' if len(badc) > 16 else ''}")
+
+
+def detail(o4, l4, r, lq, G):
+    """first sequence, kv head 0: kernel rows 32..39 -> LSE, first values, nearest ref row"""
+    sq = lq[0]
+    for kr in range(32, min(40, sq * G)):
+        pos, gg = kr // G, kr % G
+        a = o4[pos, gg].float()
+        dist = ((r[:sq, gg].float() - a) ** 2).sum(-1)
+        print(f"    row {kr}: lse4={l4[gg, pos].item():.4f} o4[:3]={a[:3].tolist()} "
+              f"ref[:3]={r[pos, gg, :3].tolist()} nearest-ref-pos={int(dist.argmin())} "
+              f"|o4|max={a.abs().max().item():.3f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--time", action="store_true")
+    ap.add_argument("--shapes", default="small")
+    ap.add_argument("--modes", default="1", help="fwd_w4 values to test (1 normal, 2 all-masked, 3 no-redo)")
+    a = ap.parse_args()
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    # (seqlens_q, seqlens_k, h, hk, causal)
+    shapes = [([128], [128], 1, 1, True), ([128], [128], 1, 1, False), ([256], [256], 1, 1, False),
+              ([113], [203], 1, 1, False), ([113], [203], 2, 1, False), ([113], [203], 4, 2, False),
+              ([64], [64], 1, 1, False), ([256], [256], 2, 2, True), ([300], [300], 2, 2, True),
+              ([1000, 700], [1000, 900], 4, 2, True), ([128], [700], 2, 1, False),
+              ([700], [128], 2, 2, True), ([513, 513], [513, 513], 3, 3, False),
+              ([2048], [2048], 2, 2, True), ([17, 300, 1], [40, 300, 5], 4, 1, False)]
+    if a.shapes == "all":
+        shapes += [([4096] * 2, [4096] * 2, 8, 8, True)]
+    worst = 0.0
+    modes = [int(x) for x in a.modes.split(",")]
+    cases = [(m, *sh) for m in modes for sh in shapes]
+    for mode, lq, lk, h, hk, causal in cases:
+        for dt in (torch.bfloat16, torch.float16):
+            q = torch.randn(sum(lq), h, 128, device=dev, dtype=dt, generator=g)
+            k = torch.randn(sum(lk), hk, 128, device=dev, dtype=dt, generator=g)
+            v = torch.randn(sum(lk), hk, 128, device=dev, dtype=dt, generator=g)
+            o8, l8 = run(q, k, v, lq, lk, causal, 0)
+            o4, l4 = run(q, k, v, lq, lk, causal, mode)
+            r = ref(q, k, v, lq, lk, causal)
+            fin = torch.isfinite(l8)
+            do = (o4.float() - o8.float()).abs().max().item()
+            e4 = (o4.float() - r).abs().max().item()
+            e8 = (o8.float() - r).abs().max().item()
+            dl = (l4[fin] - l8[fin]).abs().max().item() if fin.any() else 0.0
+            same_inf = bool(((~torch.isfinite(l4)) == (~fin)).all())
+            worst = max(worst, do)
+            print(f"m{mode} lq{lq} lk{lk} h{h} hk{hk} causal={causal} {str(dt)[6:]}: |o4-o8|={do:.3e} "
+                  f"|o4-ref|={e4:.3e} |o8-ref|={e8:.3e} |dLSE|={dl:.3e} inf-match={same_inf} "
+                  f"nan4={torch.isnan(o4).any().item()}", flush=True)
+            if do > 1e-2:
+                where((o4.float() - o8.float()).abs(), lq, h // hk)
+                if lq == [128] and lk == [128]:
+                    detail(o4, l4, r, lq, h // hk)
+    print("WORST", worst, flush=True)
+    if worst > 0.05:
+        sys.exit(1)
+    if a.time:
+        q, k, v = (torch.randn(4, 4096, 32, 128, device=dev, dtype=torch.bfloat16, generator=g)
+                   for _ in range(3))
+        fl = 4 * 4 * 32 * 4096 * 4096 * 128 / 2
+        for w4 in (0, 1, 0, 1):
+            opt("fwd_w4", w4)
+            out = torch.empty_like(q)
+            f = lambda: pa.fwd(q, k, v, out, None, 0.0, 128 ** -0.5, True, -1, -1, 0.0, False, None)  # noqa
+            t0 = time.time()
+            while time.time() - t0 < 1.0:
+                f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            print(f"C2 causal fwd_w4={w4}: {ms:.4f} ms  {fl / ms / 1e9:.1f} TFLOP/s "
+                  f"splits={capi.lib().fmha_last_num_splits()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -96,6 +96,26 @@ def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     return so
 
 
+def build_c_smoke(force: bool = False) -> str:
+    """tests/bin/c_smoke: the torch-free C++ caller of the C ABI (tests/c_smoke.cpp), linked only
+    against libpaged-attention.so (rpath to the in-tree lib/)."""
+    src = os.path.join(ROOT, "tests", "c_smoke.cpp")
+    out_dir = os.path.join(ROOT, "tests", "bin")
+    out = os.path.join(out_dir, "c_smoke")
+    so = os.path.join(LIB, LIBNAME)
+    if not os.path.exists(src):
+        return ""
+    if not force and _newer(out, [src, so, os.path.join(INCLUDE, "paged_attn.h")]):
+        return out
+    os.makedirs(out_dir, exist_ok=True)
+    cmd = [HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, src, "-o", out,
+           f"-L{LIB}", "-l:" + LIBNAME, "-Wl,-rpath,$ORIGIN/../../xf_flash_attention_cutlass_amd/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"c_smoke build failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def ext_path() -> str:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
     return os.path.join(LIB, "paged_attn" + suffix)
@@ -138,6 +158,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     so = build_lib(a.jobs, a.force, a.verbose)
     print("built", so)
+    print("built", build_c_smoke(a.force))
     if not a.no_ext:
         print("built", build_ext(a.force, a.verbose))
 

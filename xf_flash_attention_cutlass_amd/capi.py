@@ -22,6 +22,8 @@ _SIGS = {
                         C.c_int, C.c_int],
     "fmha_page_kvcache_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                               i32, vp, f32, C.c_int, C.c_int, i32, vp, vp, vp, b_, b_, b_],
+    "fmha_fwd_strided": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
+                         C.POINTER(C.c_int64), f32, C.c_int, C.c_int, f32, b_, C.c_int, vp],
     "fmha_fwd_fp8": [vp, vp, vp, vp, vp, f32, f32, f32, i32, i32, i32, i32, i32, i32, f32,
                      C.c_int, C.c_int, b_, vp],
     "fmha_varlen_fwd_ex": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,

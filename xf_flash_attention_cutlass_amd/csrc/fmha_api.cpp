@@ -205,6 +205,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.device = current_device();
     p.num_cus = num_cus(p.device);
     p.waves = o.fwd_waves.load();
+    p.fwd4 = o.fwd_w4.load();
     p.persist_per_cu = o.fwd_persistent.load();
     p.order = o.fwd_order.load();
     p.xcdq = o.fwd_xcdq.load();
@@ -265,7 +266,7 @@ extern "C" {
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
-const char* fmha_version(void) { return "xf-fmha-gfx950 1.0"; }
+const char* fmha_version(void) { return "xf-fmha-gfx950 2.0"; }
 
 int fmha_set_option(const char* name, int value) {
     clear_error();
@@ -279,7 +280,7 @@ int fmha_set_option(const char* name, int value) {
         {"fwd_xcdq", &o.fwd_xcdq, 0, 1},         {"fwd_pipe", &o.fwd_pipe, 0, 2},
         {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
-        {"dec_mr", &o.dec_mr, 16, 32},
+        {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 3},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -302,7 +303,7 @@ int fmha_get_option(const char* name) {
 #define XFA_GET(n) if (!strcmp(name, #n)) return o.n.load();
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
-    XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr)
+    XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;
@@ -337,6 +338,48 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
         run_fwd(p, !is_fp16, stream, num_splits);
     } catch (...) {
         fail(9, "internal error in fmha_fwd");
+    }
+}
+
+void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, void* softmax_lse,
+                      int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
+                      int32_t num_heads_k, int32_t head_size, const int64_t* st,
+                      float softmax_scale, int window_size_left, int window_size_right,
+                      float softcap, bool is_fp16, int num_splits, hipStream_t stream) {
+    try {
+        clear_error();
+        if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
+        REQUIRE(st != nullptr, "strides must be non-null");
+        REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
+        for (int i = 0; i < 12; ++i) REQUIRE(st[i] >= 0, "strides must be non-negative");
+        // one sequence's slab of each tensor, addressed with 32-bit offsets by the kernels
+        auto slab = [&](const char* what, int rows, int64_t row, int64_t head, int heads) {
+            const int64_t bytes = ((int64_t)(rows - 1) * row + (int64_t)(heads - 1) * head + head_size) * 2;
+            if (bytes < kMaxSlabBytes) return true;
+            return fail(1, "%s: one sequence spans %lld bytes; this build addresses a sequence with "
+                        "32-bit offsets and supports < %lld bytes", what, (long long)bytes,
+                        (long long)kMaxSlabBytes);
+        };
+        if (!slab("q", seqlen_q, st[1], st[2], num_heads) || !slab("k", seqlen_k, st[4], st[5], num_heads_k) ||
+            !slab("v", seqlen_k, st[7], st[8], num_heads_k) || !slab("o", seqlen_q, st[10], st[11], num_heads)) return;
+        FwdParams p{};
+        p.q = q; p.k = k; p.v = v; p.o = o;
+        p.lse = (float*)softmax_lse;
+        p.q_batch = st[0]; p.q_row = st[1]; p.q_head = st[2];
+        p.k_batch = st[3]; p.k_row = st[4]; p.k_head = st[5];
+        p.v_batch = st[6]; p.v_row = st[7]; p.v_head = st[8];
+        p.o_batch = st[9]; p.o_row = st[10]; p.o_head = st[11];
+        p.lse_batch = (int64_t)num_heads * seqlen_q; p.lse_head = seqlen_q;
+        p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
+        p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
+        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.wl = window_size_left; p.wr = window_size_right;
+        set_scales(p, softmax_scale, softcap);
+        p.alibi = (const float*)alibi_slopes;
+        p.alibi_bstride = batch_size > 1 ? num_heads : 0;
+        run_fwd(p, !is_fp16, stream, num_splits);
+    } catch (...) {
+        fail(9, "internal error in fmha_fwd_strided");
     }
 }
 
@@ -564,8 +607,11 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
 
 
 // ------------------------------------------------------------------ backward -----------
-// Workspace: fp32 dq_accum [tokens][h][HD] (deterministic: one such slice per key block of the
-// longest sequence) + fp32 D = rowsum(dO*O) [tokens][h].
+// Workspace: fp32 dq_accum [tokens][h][HD] (deterministic: one such slice per 256-key block of
+// the longest sequence, summed in key-block order by the convert kernel — NOT the reference's
+// split count ceil(CUs / (b*h)) of export.cpp:1090-1091, so it grows with seqlen_k; capped at
+// kMaxDetWorkspace with an error) + fp32 D = rowsum(dO*O) [tokens][h].
+constexpr size_t kMaxDetWorkspace = (size_t)32 << 30;
 static int bwd_block_n_host(int d) { return hd_bucket(d) > 128 ? 128 : 256; }
 static int bwd_slices(int max_seqlen_k, int d, bool det) {
     return det ? (max_seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d) : 1;
@@ -633,6 +679,10 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
             !bwd_rows_ok((int64_t)batch_size * seqlen_q, h, d)) return;
         const int slices = bwd_slices(seqlen_k, d, deterministic);
         const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d, slices);
+        REQUIRE(!deterministic || need <= kMaxDetWorkspace,
+                "deterministic backward needs %zu bytes of dQ slices (one per 256-key block of seqlen_k "
+                "%d); the limit is %zu: use deterministic=False for this shape", need, seqlen_k,
+                kMaxDetWorkspace);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
@@ -687,9 +737,14 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         const int h = num_heads, hk = num_heads_k, d = head_size;
         if (!slab_ok("q/out/dout/dq", max_seqlen_q, (int64_t)h * d, 2) ||
             !slab_ok("k/v/dk/dv", max_seqlen_k, (int64_t)hk * d, 2) ||
+            !slab_ok("dq_accum", max_seqlen_q, hd_bucket(d), 4) ||
             !bwd_rows_ok(total_q, h, d)) return;
         const int slices = bwd_slices(max_seqlen_k, d, deterministic);
         const size_t need = bwd_ws_bytes(total_q, h, d, slices);
+        REQUIRE(!deterministic || need <= kMaxDetWorkspace,
+                "deterministic backward needs %zu bytes of dQ slices (one per 256-key block of "
+                "max_seqlen_k %d); the limit is %zu: use deterministic=False for this shape", need,
+                max_seqlen_k, kMaxDetWorkspace);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);

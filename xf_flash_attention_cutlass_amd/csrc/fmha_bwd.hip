@@ -34,13 +34,13 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
                : (feat ? fmha_bwd_kernel<HD, T, false, true> : fmha_bwd_kernel<HD, T, false, false>);
     const size_t smem = bwd_smem_bytes<HD>();
     static std::atomic<unsigned long long> attr_done{0};
-    if (first_on_device(attr_done, p.device)) {
+    once_per_device(attr_done, p.device, [&] {
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    }
+    });
     const dim3 grid(p.b * p.hk, (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>());
     hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, p);
     e = hipGetLastError();

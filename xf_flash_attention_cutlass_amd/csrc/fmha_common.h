@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <mutex>
 #include <type_traits>
 
 namespace xfa {
@@ -23,11 +24,19 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // Per-device one-time host action (kernel attributes are set per device: a process may drive
-// several GPUs).  Returns true exactly once per (flag word, device) for devices 0..63.
-inline bool first_on_device(std::atomic<unsigned long long>& done, int device) {
-    if (device < 0 || device >= 64) return true;
+// several GPUs).  `apply` runs once per (flag word, device) for devices 0..63 (always for
+// others); the device's bit is set only after `apply` has returned, so a concurrent caller on
+// the same device waits for it instead of launching before the attributes are in place.
+template <typename F>
+inline void once_per_device(std::atomic<unsigned long long>& done, int device, F&& apply) {
+    if (device < 0 || device >= 64) { apply(); return; }
     const unsigned long long bit = 1ull << device;
-    return !(done.fetch_or(bit) & bit);
+    if (done.load(std::memory_order_acquire) & bit) return;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.load(std::memory_order_relaxed) & bit) return;
+    apply();
+    done.fetch_or(bit, std::memory_order_release);
 }
 
 // ------------------------------------------------------------------ vector types --
@@ -118,6 +127,7 @@ struct FwdParams {
     int order;                 // persistent item order (0 boustrophedon, 1 XCD-grouped pairs)
     int xcdq;                  // dynamic queue kind (1 per-XCD queues)
     int device;                // current device id (per-device one-time kernel attributes)
+    int fwd4;                  // 1: the 4-wave D = 128 forward where eligible (fmha_fwd4_kernel.h)
 };
 
 struct CombineParams {

@@ -3,6 +3,9 @@
 // keeps the per-variant kernels in separate code objects (co-compiled template variants
 // perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
 #include "fmha_fwd_kernel.h"
+#if XFA_HD == 128
+#include "fmha_fwd4_kernel.h"
+#endif
 #include "fmha_decode_kernel.h"
 #include "fmha_launch.h"
 
@@ -46,12 +49,12 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
         constexpr int NWV = 2 * kDecWaves;
         const size_t smem = (size_t)NWV * 2 * kDecKeys * HD * 2;
         static std::atomic<unsigned long long> attr_done{0};
-        if (first_on_device(attr_done, p.device)) {
+        once_per_device(attr_done, p.device, [&] {
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, true, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 32, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, true, 16, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 16, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        }
+        });
         const dim3 grid(p.b * p.hk / NWV, p.num_splits);
         if (p.dec_mr == 16) {
             if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16, NWV>), grid, dim3(NWV * 64), smem, st, p);
@@ -101,17 +104,47 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         mask ? (feat ? fmha_fwd_kernel<HD, T, NW, true, true> : fmha_fwd_kernel<HD, T, NW, true, false>)
              : (feat ? fmha_fwd_kernel<HD, T, NW, false, true> : fmha_fwd_kernel<HD, T, NW, false, false>);
     static std::atomic<unsigned long long> attr_done{0};
-    if (first_on_device(attr_done, p.device)) {
+    once_per_device(attr_done, p.device, [&] {
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    }
+    });
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
 }
+
+#if XFA_HD == 128
+// 4-wave forward (fmha_fwd4_kernel.h): dense / varlen, D = 128, one split, no left
+// window, no ALiBi / softcap / paged / fp8 K/V / leftpad (those run the 8-wave kernel)
+static bool fwd4_eligible(const FwdParams& p) {
+    return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 &&
+           (p.wl < 0 || p.wl >= p.seqlen_k) && !p.alibi &&
+           !(p.softcap_pre > 0.f) && !p.block_table && !p.kv_fp8 && !p.leftpad_k;
+}
+
+static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
+    const int n_mb = (p.seqlen_q * p.group + kFwd4Rows - 1) / kFwd4Rows;
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    dim3 grid(p.b * p.hk, n_mb, 1);
+    const int items = p.b * p.hk * n_mb;
+    const int slots = p.num_cus;
+    if (p.persist_per_cu > 0 && items > slots) {
+        pp.persistent = p.work_ctr ? 3 : (p.order == 1 && slots % 8 == 0) ? 2 : 1;
+        pp.xcd_queues = p.work_ctr && p.xcdq && slots % 8 == 0 && p.b * p.hk >= 8;
+        grid = dim3(slots, 1, 1);
+    }
+    constexpr bool BF = std::is_same<elem_t, __bf16>::value;
+    static std::atomic<unsigned long long> attr_done{0};
+    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd4_kernel<BF>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd4Smem); });
+    hipLaunchKernelGGL((fmha_fwd4_kernel<BF>), grid, dim3(256), kFwd4Smem, st, pp);
+    return hipGetLastError();
+}
+#endif
 
 hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
 #if XFA_HD > 128
@@ -119,6 +152,9 @@ hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
     return launch_fwd_nw<XFA_HD, elem_t, 4>(p, st);
 #else
     if (p.decode) return launch_decode<XFA_HD, elem_t>(p, st);
+#if XFA_HD == 128
+    if (fwd4_eligible(p)) return launch_fwd4(p, st);
+#endif
     if (p.waves == 8) return launch_fwd_nw<XFA_HD, elem_t, 8>(p, st);
     return launch_fwd_nw<XFA_HD, elem_t, 4>(p, st);
 #endif

@@ -26,10 +26,10 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
     const size_t smem = 8 * (size_t)kFp8Tile;     // K and V, four buffers each
     void (*kern)(const FwdParams) = mask ? fmha_fwd_fp8_kernel<T, NW, true> : fmha_fwd_fp8_kernel<T, NW, false>;
     static std::atomic<unsigned long long> attr_done{0};
-    if (first_on_device(attr_done, p.device)) {
+    once_per_device(attr_done, p.device, [&] {
         (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    }
+    });
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     return hipGetLastError();
 }

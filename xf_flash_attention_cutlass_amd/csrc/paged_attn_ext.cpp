@@ -96,9 +96,12 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     CHECK_SHAPE(k, batch_size, seqlen_k, num_heads_k, head_size_og);
     CHECK_SHAPE(v, batch_size, seqlen_k, num_heads_k, head_size_og);
 
-    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
-    at::Tensor k_padded = pad_last(k, head_size_og).contiguous();
-    at::Tensor v_padded = pad_last(v, head_size_og).contiguous();
+    // d % 8 == 0: strided views (head / batch slices) run in place through fmha_fwd_strided;
+    // otherwise the reference's padding to a multiple of 8 (export.cpp:539-547)
+    const bool strided = head_size_og % 8 == 0;
+    at::Tensor q_padded = strided ? q : pad_last(q, head_size_og).contiguous();
+    at::Tensor k_padded = strided ? k : pad_last(k, head_size_og).contiguous();
+    at::Tensor v_padded = strided ? v : pad_last(v, head_size_og).contiguous();
     at::Tensor out;
     if (out_.has_value()) {
         out = out_.value();
@@ -106,9 +109,9 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
         CHECK_DEVICE(out);
         TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
         CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size_og);
-        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+        if (head_size_og % 8 != 0) out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
     } else {
-        out = torch::empty_like(q_padded);
+        out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
     }
     const int head_size = round8(head_size_og);
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
@@ -119,7 +122,17 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
 
-    if (seqlen_k > 0) {
+    if (seqlen_k > 0 && strided) {
+        const int64_t st[12] = {q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1),
+                                k.stride(2), v.stride(0), v.stride(1), v.stride(2), out.stride(0),
+                                out.stride(1), out.stride(2)};
+        fmha_fwd_strided(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(),
+                         alibi.defined() ? alibi.data_ptr() : nullptr, softmax_lse.data_ptr(),
+                         seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, head_size, st,
+                         softmax_scale, window_size_left, window_size_right, softcap,
+                         q.dtype() == torch::kFloat16, 0, cur_stream());
+        raise_if_failed("fwd");
+    } else if (seqlen_k > 0) {
         fmha_fwd(q_padded.data_ptr(), k_padded.data_ptr(), v_padded.data_ptr(), out.data_ptr(),
                  alibi.defined() ? alibi.data_ptr() : nullptr, seqlen_q, seqlen_k, batch_size,
                  num_heads, num_heads_k, head_size, p_dropout, cur_stream(), nullptr, softmax_scale,

@@ -53,6 +53,11 @@ def flash_attn_func(q, k, v, dropout_p=0.0, causal=False, window_size=(-1, -1), 
     if softmax_scale is None:
         softmax_scale = q.shape[-1] ** (-0.5)
     if q.dtype == torch.float8_e4m3fn:
+        # the fp8 forward has no dropout / softcap / ALiBi: refuse instead of dropping them
+        if dropout_p != 0.0 or softcap != 0.0 or alibi_slopes is not None:
+            raise NotImplementedError("fp8 q/k/v: dropout, softcap and ALiBi are not supported "
+                                      f"(dropout_p={dropout_p}, softcap={softcap}, "
+                                      f"alibi={'set' if alibi_slopes is not None else None})")
         out, lse = flash_attn_fp8_func(q, k, v, q_descale, k_descale, v_descale, softmax_scale,
                                        causal, window_size, out_dtype, return_lse=True)
         return out if not return_attn_probs else (out, lse, None)

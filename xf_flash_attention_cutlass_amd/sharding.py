@@ -125,17 +125,16 @@ def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
         qs, ks = shards[rank]
         if alibi is not None:
             kw["alibi_slopes"] = _slice_alibi(alibi, heads=qs)
-        out_local = local_fn(q[:, :, qs.start:qs.stop].contiguous(),
-                             k[:, :, ks.start:ks.stop].contiguous(),
-                             v[:, :, ks.start:ks.stop].contiguous(), **kw)
+        # head-sliced views go to the kernels as they are (fmha_fwd_strided): no copies
+        out_local = local_fn(q[:, :, qs.start:qs.stop], k[:, :, ks.start:ks.stop],
+                             v[:, :, ks.start:ks.stop], **kw)
         if not gather:
             return out_local, qs
         return all_gather_dim(out_local, [a.size for a, _ in shards], 2), qs
     bs = shards[rank]
     if alibi is not None:
         kw["alibi_slopes"] = _slice_alibi(alibi, batch=bs)
-    out_local = local_fn(q[bs.start:bs.stop].contiguous(), k[bs.start:bs.stop].contiguous(),
-                         v[bs.start:bs.stop].contiguous(), **kw)
+    out_local = local_fn(q[bs.start:bs.stop], k[bs.start:bs.stop], v[bs.start:bs.stop], **kw)
     if not gather:
         return out_local, bs
     return all_gather_dim(out_local, [s.size for s in shards], 0), bs
