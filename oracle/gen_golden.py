@@ -5,11 +5,14 @@ reference's own pure-PyTorch oracle functions out of /root/reference/test.py by
 AST extraction (the module itself cannot be imported: it dlopens a DCU .so and
 imports the absent third-party `flash_attn` at import time, test.py:15-31), runs
 the reference's test recipes (seeds, shapes, windows, padding, paged caches) on
-CPU and stores inputs + the reference's outputs (`out_ref` = upcast fp32 oracle,
-`out_pt` = low-precision PyTorch estimate) as small safetensors files.
+CPU and stores the reference's outputs (`out_ref` = upcast fp32 oracle, its gradients, and
+for paged cases `out_pt` = the low-precision estimate) as small safetensors files.  The seeded
+random inputs are not stored: their SHA-256 and the recipe are, and tests/golden_util.py
+regenerates them (and recomputes the pinned low-precision twin) at load time.
 
 It also checks that our restatement in `oracle/attention_ref.py` reproduces the
-reference functions bit for bit on every case (this is what pins the oracle).
+reference functions bit for bit on every case — outputs of both twins and, for the
+forward cases, their autograd gradients (this is what pins the oracle).
 
 Usage:  python oracle/gen_golden.py [--check-only]
 """
@@ -54,10 +57,17 @@ def _grads(out, inputs, g):
     return torch.autograd.grad(out, inputs, g)
 
 
-def _save(name, tensors, meta):
+def _save(name, tensors, meta, regen=(), derived=()):
+    """Store the case; the seeded inputs in `regen` are dropped and recorded by SHA-256 (the
+    tests regenerate them by the same recipe, tests/golden_util.py), `derived` tensors (the
+    low-precision twin, pinned bit for bit above) are dropped and recomputed by the tests."""
     from safetensors.torch import save_file
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import digest
     os.makedirs(GOLDEN, exist_ok=True)
     tensors = {k: v.detach().contiguous().cpu() for k, v in tensors.items() if v is not None}
+    meta = dict(meta, sha256={k: digest(tensors[k]) for k in regen if k in tensors})
+    tensors = {k: v for k, v in tensors.items() if k not in regen and k not in derived}
     save_file(tensors, os.path.join(GOLDEN, name + ".safetensors"),
               metadata={"meta": json.dumps(meta)})
 
@@ -105,11 +115,20 @@ def case_fwd(ref, name, *, b, h, hk, sq, sk, d, dtype, causal, local=False, alib
         g = torch.randn_like(out_ref)
         dq, dk, dv = _grads(out_ref, (qg, kg, vg), g)
         t.update(dout=g, dq_ref=dq, dk_ref=dk, dv_ref=dv)
+        # pin the restatement's gradients too (both twins) against the reference's autograd
+        ref_pt = _grads(out_pt, (qg, kg, vg), g)
+        for upcast, want in ((True, (dq, dk, dv)), (False, ref_pt)):
+            mq, mk, mv = (x.clone().requires_grad_(True) for x in (q, k, v))
+            mo, _ = ours.attention_ref(mq, mk, mv, None, None, bias, 0.0, None, causal=causal,
+                                       window_size=window, softcap=softcap, upcast=upcast,
+                                       reorder_ops=not upcast)
+            for n, a, r in zip(("dq", "dk", "dv"), _grads(mo, (mq, mk, mv), g), want):
+                _same(a, r, f"{name}:{n}_{'ref' if upcast else 'pt'}")
     meta = dict(kind="fwd", b=b, h=h, hk=hk, sq=sq, sk=sk, d=d, dtype=str(dtype).split(".")[-1],
                 causal=causal, window=list(window), alibi=alibi, softcap=softcap,
                 recipe="test.py:751-986 (test_flash_attn_output), CPU, manual_seed(0)")
     if save:
-        _save(name, t, meta)
+        _save(name, t, meta, regen=("q", "k", "v", "alibi_slopes", "dout"), derived=("out_pt",))
     return t
 
 
@@ -129,12 +148,15 @@ def case_varlen(ref, name, *, b, h, hk, sq, sk, d, dtype, causal, local=False):
     mine, _ = ours.attention_ref(q, k, v, qpm, kpm, None, 0.0, None, causal=causal,
                                  window_size=window)
     _same(mine, out_ref, name + ":out_ref")
+    mine_pt, _ = ours.attention_ref(q, k, v, qpm, kpm, None, 0.0, None, causal=causal,
+                                    window_size=window, upcast=False, reorder_ops=True)
+    _same(mine_pt, out_pt, name + ":out_pt")
     t = dict(q=q, k=k, v=v, query_padding_mask=qpm, key_padding_mask=kpm,
              out_ref=out_ref, out_pt=out_pt)
     meta = dict(kind="varlen", b=b, h=h, hk=hk, sq=sq, sk=sk, d=d,
                 dtype=str(dtype).split(".")[-1], causal=causal, window=list(window),
                 recipe="test.py:1026-1307 (test_flash_attn_varlen_output), CPU, manual_seed(0)")
-    _save(name, t, meta)
+    _save(name, t, meta, regen=("q", "k", "v"), derived=("out_pt",))
 
 
 def case_kvcache(ref, name, *, b, h, hk, sq, sk, d, dtype, causal=False, local=True,
@@ -162,7 +184,7 @@ def case_kvcache(ref, name, *, b, h, hk, sq, sk, d, dtype, causal=False, local=T
                 num_blocks=nblocks, num_splits=num_splits, dtype=str(dtype).split(".")[-1],
                 causal=causal, window=list(window),
                 recipe="test.py:1355-1594 (test_flash_attn_kvcache), paged, CPU, manual_seed(0)")
-    _save(name, t, meta)
+    _save(name, t, meta, regen=("q",))
 
 
 def _compact_pool(kp, vp, table, cache_seqlens, page):

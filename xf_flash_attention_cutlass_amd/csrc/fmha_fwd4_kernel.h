@@ -178,10 +178,17 @@ __device__ __forceinline__ void fwd4_item(const FwdParams& p, char* smem, const 
 
 // Persistent grid (one workgroup per CU) walking (b x kv head, row block) items in the
 // 8-wave kernel's orders: XCD-grouped pairs (dense) or per-XCD dynamic queues (varlen).
+#ifdef XFA_FWD4_STAMP
+static __device__ unsigned long long g_fwd4_stamp[4];
+#endif
 template <bool BF16>
 __global__ void __launch_bounds__(256, 1) fmha_fwd4_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_claim[2];
+#ifdef XFA_FWD4_STAMP
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_in = 0;
+#endif
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
     for (int k = 0;; ++k) {
@@ -220,8 +227,21 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd4_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
+#ifdef XFA_FWD4_STAMP
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         fwd4_item<BF16>(p, smem, bh, m_block);
+        t_in += __builtin_amdgcn_s_memtime() - t1;
+#else
+        fwd4_item<BF16>(p, smem, bh, m_block);
+#endif
     }
+#ifdef XFA_FWD4_STAMP
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_fwd4_stamp[0], t_in);
+        atomicAdd(&g_fwd4_stamp[1], __builtin_amdgcn_s_memtime() - t_start);
+        atomicAdd(&g_fwd4_stamp[2], 1ull);
+    }
+#endif
     if (p.persistent == 3 && threadIdx.x == 0) {
         const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
         if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {
