@@ -281,6 +281,7 @@ int fmha_set_option(const char* name, int value) {
         {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 3},
+        {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -304,6 +305,7 @@ int fmha_get_option(const char* name) {
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
     XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
+    XFA_GET(bwd_order) XFA_GET(bwd_desc)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;
@@ -656,6 +658,8 @@ static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl,
     p.scale_log2 = scale_softmax * 1.4426950408889634f;
     p.alibi_mul = 1.f / scale_softmax;
     p.device = current_device();
+    p.order = options().bwd_order.load();
+    p.desc = options().bwd_desc.load();
     return true;
 }
 

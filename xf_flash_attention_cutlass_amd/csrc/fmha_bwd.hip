@@ -41,8 +41,11 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     });
-    const dim3 grid(p.b * p.hk, (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>());
-    hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, p);
+    const int nkb = (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>();
+    BwdParams pp = p;
+    pp.order = p.order && (p.b * p.hk) % 8 == 0;
+    const dim3 grid = pp.order ? dim3(p.b * p.hk * nkb) : dim3(p.b * p.hk, nkb);
+    hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, pp);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((fmha_bwd_convert_kernel<HD, T>), dim3(blocks), dim3(256), 0, st, p, total_rows);

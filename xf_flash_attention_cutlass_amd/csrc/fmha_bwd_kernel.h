@@ -215,10 +215,18 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     const int lr = lane & 31;
     const int hh = lane >> 5;
 
-    const int bh = blockIdx.x;
+    // order 1: workgroup w runs on XCD w % 8 (dispatch round-robin); XCD x takes the kv heads
+    // bh = x (mod 8), each with its key blocks consecutive, heaviest (causal) first
+    int bh = blockIdx.x, kb = blockIdx.y;
+    if (p.order) {
+        const int nkb = (p.seqlen_k + BN - 1) / BN;
+        const int i = (int)(blockIdx.x >> 3);
+        bh = (int)(blockIdx.x & 7) + 8 * (i / nkb);
+        kb = i - (i / nkb) * nkb;
+    }
     const int bidx = bh / p.hk;
     const int hk_i = bh - bidx * p.hk;
-    const int n0 = blockIdx.y * BN;
+    const int n0 = kb * BN;
 
     int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
     if (FEAT) {
@@ -289,7 +297,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     auto lsd_value = [&]() { return hh ? (lsd_ok ? lsd_raw : 0.f) : (lsd_ok ? lsd_raw * kLog2e : INFINITY); };
     auto load_q = [&](int it) {
         const int g = it / ntiles;
-        const int tt = it - g * ntiles;
+        const int tt = p.desc ? (g + 1) * ntiles - 1 - it : it - g * ntiles;
         const int head = hk_i * G + g;
         {
             const int pos = (t_lo + tt) * BQ + lr;
@@ -390,7 +398,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
-    float* const dq_base = p.dq_accum + (DET ? (int64_t)blockIdx.y * p.acc_slice : 0);
+    float* const dq_base = p.dq_accum + (DET ? (int64_t)kb * p.acc_slice : 0);
     float lsd_cur = 0.f;
     float* const lsd_slot = reinterpret_cast<float*>(ds_lds + wave * kBwdKeysPerWave * 64);
     if (n_iter > 0) { load_q(0); }
@@ -400,7 +408,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 
     for (int it = 0; it < n_iter; ++it) {
         const int g = it / ntiles;
-        const int tt = it - g * ntiles;
+        const int tt = p.desc ? (g + 1) * ntiles - 1 - it : it - g * ntiles;
         const int head = hk_i * G + g;
         const int q0 = (t_lo + tt) * BQ;
         // this tile's LSE / D -> a private slot in this wave's own dS^T rows (nobody reads

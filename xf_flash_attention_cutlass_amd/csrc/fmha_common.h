@@ -174,6 +174,8 @@ struct BwdParams {
     int dq_slices;       // deterministic: dQ partials per key block in dq_accum slices (0 = atomics)
     int64_t acc_slice;   // floats between dq_accum slices
     int device;          // current device id (per-device one-time kernel attributes)
+    int order;           // 1: 1-D grid, the key blocks of one (batch, kv head) consecutive on one XCD
+    int desc;            // 1: each key block sweeps its query tiles last to first
 };
 
 // ------------------------------------------------------------------ dtype traits --

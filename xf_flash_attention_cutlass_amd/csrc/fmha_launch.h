@@ -28,6 +28,11 @@ struct Options {
     std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
     std::atomic<int> dec_mr{16};         // decode MFMA rows: 16 when the query rows fit 16 (C5: 105 vs
                                          // 110 us with dec_hmaj = 1), else 32
+    std::atomic<int> bwd_order{0};       // backward grid: 1 = the key blocks of one (b, kv head) consecutive
+                                         // on one XCD (they then sweep the same Q / dO tiles together;
+                                         // C3: 3.03 vs 2.88 ms - their dQ atomics then collide)
+    std::atomic<int> bwd_desc{0};        // backward query-tile sweep: 1 = last tile first (C3: 2.86 vs
+                                         // 2.88 ms, within noise)
     std::atomic<int> dec_hmaj{1};        // decode workgroup: 0 = 1 kv head x 4 splits, 1 = 4 kv heads x one
                                          // split, 2 = 8 kv heads x one split (C5 fp8: 116 / 110 / 112 us)
 };
