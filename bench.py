@@ -3,8 +3,10 @@
 Workloads (BASELINE.json configs):
   --mode fwd     (default) C2: mha_fwd B=4 H=32 S=4096 D=128 bf16 causal; one step = one
                  forward over the batch.  The default line also carries driver-timed
-                 sub-results for C3 ("fwd_bwd"), C4 ("varlen") and C5 ("decode"), each with its
-                 own roofline, because the metric names fwd and fwd+bwd and BASELINE lists all.
+                 sub-results for C3 ("fwd_bwd"), C4 ("varlen"), C5 ("decode", full caches, and
+                 "decode_ragged", cache lengths U[1, 32768]) and the fp8 forward, each with its
+                 own roofline and CPU baseline (median of 3 runs), because the metric names fwd
+                 and fwd+bwd and BASELINE lists all.
   --mode fwdbwd  C3: mha_fwd + mha_bwd, same shape (FLOPs = 3.5 x fwd, the usual convention).
   --mode varlen  C4: mha_varlen_fwd, 32 ragged sequences, total 131072 tokens, H=32 D=128 bf16.
   --mode decode  C5: paged-KV decode (fwd_kvcache), per GPU B=8 H=32 Hk=8 Sq=1, cache 32768
@@ -78,7 +80,8 @@ def parse(argv=None):
                     help="input sets cycled step by step (default: 2 for fwd/fwdbwd, so every "
                          "step reads inputs last touched two steps ago; C4/C5 inputs exceed the "
                          "256 MiB Infinity Cache on their own)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=6.0,
+                    help="CPU budget per baseline (split over 3 runs; the median is reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the C3/C4/C5 sub-results of the default (fwd) line")
@@ -113,51 +116,86 @@ def _host():
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline_dense(heads: int, s: int, d: int, causal: bool, budget_s: float):
-    """Reference CPU eager path (oracle restatement of test.py:310-397, fp32 upcast) timed on
-    the host cores over a bounded sample: repeated (1 batch x `heads` heads) chunks of the
-    same workload until `budget_s` seconds of work; reported in TFLOP/s."""
+def _median_runs(run, reps, budget_s):
+    """`reps` timed runs of `run(budget)` (each returns (units, seconds, sample)), the median
+    rate and every run's rate (median of >= 3 runs)."""
+    rates, sample = [], ""
+    for _ in range(reps):
+        units, el, sample = run(budget_s / reps)
+        rates.append(units / el)
+    rates.sort()
+    return rates[len(rates) // 2], rates, sample
+
+
+def cpu_baseline_dense(heads: int, s: int, d: int, causal: bool, budget_s: float,
+                       backward: bool = False, reps: int = 3):
+    """Reference CPU eager path (oracle restatement of test.py:310-397, fp32 upcast; with
+    `backward` also its autograd backward, FLOPs 3.5 x fwd as the GPU line counts) timed on
+    the host cores: `reps` runs over a bounded sample of repeated (1 batch x `heads` heads)
+    chunks of the same workload; the median run in TFLOP/s."""
     from oracle import attention_ref as orc
     threads = _threads()
     g = torch.Generator().manual_seed(0)
     q, k, v = (torch.randn(1, s, heads, d, generator=g).bfloat16() for _ in range(3))
+    do = torch.randn(1, s, heads, d, generator=g).bfloat16()
     orc.attention_ref(q[:, :256], k[:, :256], v[:, :256], causal=causal)   # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc.attention_ref(q, k, v, causal=causal)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 50:
-            break
-    flops = n * fwd_flops(1, heads, s, s, d, causal)
-    return {"value": round(flops / el / 1e12, 4), "unit": "TFLOP/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} x attention_ref(1x{s}x{heads}x{d} bf16->fp32, causal={causal}) "
-                      f"in {el:.1f}s on {_host()}"}
+
+    def one():
+        if not backward:
+            orc.attention_ref(q, k, v, causal=causal)
+            return
+        qq, kk, vv = (x.clone().requires_grad_(True) for x in (q, k, v))
+        out, _ = orc.attention_ref(qq, kk, vv, causal=causal)
+        torch.autograd.grad(out, (qq, kk, vv), do)
+
+    def run(budget):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            one()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 50:
+                break
+        fl = n * fwd_flops(1, heads, s, s, d, causal) * (3.5 if backward else 1.0)
+        return fl, el, f"{n} x attention_ref{'+autograd bwd' if backward else ''}" \
+                       f"(1x{s}x{heads}x{d} bf16->fp32, causal={causal})"
+
+    if backward:
+        qq, kk, vv = (x[:, :256].clone().requires_grad_(True) for x in (q, k, v))
+        out, _ = orc.attention_ref(qq, kk, vv, causal=causal)      # autograd warm-up
+        torch.autograd.grad(out, (qq, kk, vv), do[:, :256])
+    med, rates, sample = _median_runs(run, reps, budget_s)
+    return {"value": round(med / 1e12, 4), "unit": "TFLOP/s", "cores": threads, "kind": "port",
+            "runs": [round(r / 1e12, 4) for r in rates], "cpu": _host(),
+            "sample": f"median of {reps} runs of ~{budget_s / reps:.1f}s, last: {sample}"}
 
 
-def cpu_baseline_decode(h: int, hk: int, s: int, d: int, budget_s: float):
+def cpu_baseline_decode(h: int, hk: int, s: int, d: int, budget_s: float, reps: int = 3):
     """Decode on the CPU oracle: one query token against an s-token cache (the fp8 cache
-    dequantised to bf16, as the reference path would hold it), repeated for `budget_s`;
-    reported as GB/s of the same algorithmic bytes the GPU line counts (fp8 K+V)."""
+    dequantised to bf16, as the reference path would hold it), `reps` runs; reported as GB/s
+    of the same algorithmic bytes the GPU line counts (fp8 K+V), median run."""
     from oracle import attention_ref as orc
     threads = _threads()
     g = torch.Generator().manual_seed(0)
     q = torch.randn(1, 1, h, d, generator=g).bfloat16()
     k, v = (torch.randn(1, s, hk, d, generator=g).bfloat16() for _ in range(2))
     orc.attention_ref(q, k[:, :256], v[:, :256])
-    n, t0 = 0, time.perf_counter()
-    while True:
-        orc.attention_ref(q, k, v)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 200:
-            break
-    nbytes = n * (2 * s * hk * d * 1 + 2 * h * d * 2)
-    return {"value": round(nbytes / el / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} x attention_ref(q 1x1x{h}x{d}, K/V 1x{s}x{hk}x{d} bf16->fp32) "
-                      f"in {el:.1f}s on {_host()}"}
+
+    def run(budget):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            orc.attention_ref(q, k, v)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 200:
+                break
+        nbytes = n * (2 * s * hk * d * 1 + 2 * h * d * 2)
+        return nbytes, el, f"{n} x attention_ref(q 1x1x{h}x{d}, K/V 1x{s}x{hk}x{d} bf16->fp32)"
+
+    med, rates, sample = _median_runs(run, reps, budget_s)
+    return {"value": round(med / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "runs": [round(r / 1e9, 3) for r in rates], "cpu": _host(),
+            "sample": f"median of {reps} runs of ~{budget_s / reps:.1f}s, last: {sample}"}
 
 
 # ----------------------------------------------------------------------------- workloads
@@ -238,7 +276,8 @@ def workload_dense(a, mode, dev, rank, world):
                         "parallelism": f"dp{world} ({a.scaling} scaling: "
                                        f"{'batch' if a.scaling == 'weak' else 'GQA-aligned head'}"
                                        f" shards, no collective in the step)"},
-                cpu=lambda: cpu_baseline_dense(8, S, D, causal, a.cpu_baseline_seconds))
+                cpu=lambda: cpu_baseline_dense(8 if mode == "fwd" else 2, S, D, causal,
+                                               a.cpu_baseline_seconds, backward=mode == "fwdbwd"))
 
 
 def workload_fp8(a, dev, rank, world):
@@ -305,8 +344,9 @@ def workload_varlen(a, dev, rank, world):
     fl = sum(fwd_flops(1, H, s, s, D, causal) for s in lens)
     cs = "causal" if causal else "non-causal"
     return dict(step=step, units=fl, bound="mfma", out=lambda: out, gather_dim=0,
-                config={"workload": f"mha_varlen_fwd 32 ragged seqs U[1024,7168] (seed 0) "
-                                    f"total=131072 H={H} D={D} bf16 {cs}",
+                config={"workload": f"mha_varlen_fwd 32 ragged seqs, lengths {min(lens)}-{max(lens)} "
+                                    f"(U[1024,7168] draw, seed {rank}, rescaled to total 131072) "
+                                    f"H={H} D={D} bf16 {cs}",
                         "global_batch": 32 * world if a.scaling == "weak" else 32,
                         "seq_len": mx, "total_tokens": tot, "heads": H, "head_dim": D,
                         "rank_shard": shard,
@@ -398,7 +438,7 @@ def measured_traffic(mode):
 
 
 def event_ms(step, steps, stream):
-    """Mean per-step time from HIP events recorded on the launch stream around every step
+    """Median per-step time from HIP events recorded on the launch stream around every step
     (a separate pass: the event records do not sit in the wall-clock timed region)."""
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
@@ -407,7 +447,8 @@ def event_ms(step, steps, stream):
         step()
         evs[i][1].record(stream)
     torch.cuda.synchronize()
-    return sum(s.elapsed_time(e) for s, e in evs) / steps
+    ts = sorted(s.elapsed_time(e) for s, e in evs)
+    return ts[len(ts) // 2]
 
 
 def prewarm(step, seconds, sync):
@@ -435,8 +476,10 @@ def roofline(w, ms, mode):
     return roof
 
 
-def sub_result(a, mode, dev, stream):
-    """A driver-timed sub-result (same method as the main line, rank-local, 1 GPU)."""
+def sub_result(a, mode, dev, stream, **over):
+    """A driver-timed sub-result (same method as the main line, rank-local, 1 GPU), with its
+    own CPU baseline; `over` overrides arguments (e.g. ragged=True)."""
+    a = argparse.Namespace(**{**vars(a), **over})
     w = build_workload(a, mode, dev, 0, 1)
     step = w["step"]
     prewarm(step, 0.5, torch.cuda.synchronize)
@@ -455,6 +498,8 @@ def sub_result(a, mode, dev, stream):
     out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
            "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
            "unit": "GB/s" if hbm else "TFLOP/s", "roofline": roofline(w, ev, mode)}
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = w["cpu"]()
     del w
     torch.cuda.empty_cache()
     return out
@@ -614,6 +659,7 @@ def main(argv=None):
         extras["fwd_bwd"] = sub_result(a, "fwdbwd", dev, stream)
         extras["varlen"] = sub_result(a, "varlen", dev, stream)
         extras["decode"] = sub_result(a, "decode", dev, stream)
+        extras["decode_ragged"] = sub_result(a, "decode", dev, stream, ragged=True)
         extras["fwd_fp8"] = sub_result(a, "fwd_fp8", dev, stream)
     if dist:
         dist.barrier()

@@ -35,10 +35,14 @@ extern "C" {
 /* Dense forward.  Replaces csrc/paged_attn.h:8-31 (impl paged_attn.cpp:310-383).
  * Writes o and, when softmax_lse_ptr != NULL, the fp32 log-sum-exp [batch, heads, seqlen_q]
  * (the reference leaves it unwritten; bwd needs it).  alibi_slopes_ptr: fp32 [heads] or
- * [batch, heads] (the latter when batch > 1, as paged_attn.cpp:375 assumes).  Dropout and
- * return_softmax are not supported on the C path (the reference's split kernel ignores them,
- * SURVEY §8a (ii)): p_dropout > 0 is rejected with an error.  num_splits <= 0 picks a split
- * count; 1 forces the single-pass kernel. */
+ * [batch, heads] (the latter when batch > 1, as paged_attn.cpp:375 assumes).  p_dropout in
+ * [0, 1): P is dropped with Philox keep bits drawn from this thread's RNG state
+ * (fmha_set_rng_state) and the kept values scaled by 1 / (1 - p_dropout), as the reference's
+ * dropout forward (dropout_hip.h:14-109, whose C path never runs it); no KV
+ * split with dropout.  return_softmax (needs p_dropout > 0, p_ptr and softmax_lse_ptr): p_ptr
+ * receives the dropped-out softmax [batch, heads, round128(seqlen_q), round128(seqlen_k)] in q's
+ * dtype, dropped entries with the sign bit set (the reference's S_dmask encoding; here P is
+ * normalised).  num_splits <= 0 picks a split count; 1 forces the single-pass kernel. */
 void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_slopes_ptr,
               const int32_t seqlen_q, const int32_t seqlen_k, const int32_t batch_size,
               const int32_t num_heads, const int32_t num_heads_k, const int32_t head_size,
@@ -87,6 +91,12 @@ int fmha_last_status(void);
  * kernel: one split per wave).  Diagnostic, for tests and tuning. */
 int fmha_last_num_splits(void);
 
+/* Dropout RNG state of the calling thread: the following forward / backward calls with
+ * p_dropout > 0 draw their keep bits from Philox4x32-7 keyed by (seed, offset) over the score
+ * coordinates (batch x head, query position, key) - a forward and the backward of the same
+ * scores with the same state drop the same entries (flash-attn's rng_state = {seed, offset}). */
+void fmha_set_rng_state(uint64_t seed, uint64_t offset);
+
 /* Library version / build identification, e.g. "xf-fmha-gfx950 2.0".  2.0 (round 3) changed
  * argument lists of existing symbols (see INTEGRATION.md "ABI history"). */
 const char* fmha_version(void);
@@ -98,7 +108,8 @@ const char* fmha_version(void);
  * query rows per forward workgroup), fwd_prio (0/1), fwd_persistent (workgroups per CU, 0 =
  * one workgroup per item), fwd_slack (0..16), fwd_order (0/1), fwd_dyn (0..2), fwd_xcdq (0/1),
  * fwd_pipe (0..2), fwd_decode (0/1), dec_wg_per_cu (1..16), dec_hmaj (0..2), dec_mr (16/32),
- * fwd_w4 (0/1: the 4-wave D = 128 forward where eligible). */
+ * fwd_w4 (0/1: the 4-wave D = 128 forward where eligible), bwd_order (0/1), bwd_desc (0/1),
+ * dec_fold (0/1: the decode split combine folded into the split launch). */
 int fmha_set_option(const char* name, int value);
 /* Current value of a knob, or -1 (with fmha_last_error set) for an unknown name. */
 int fmha_get_option(const char* name);
@@ -114,12 +125,14 @@ int fmha_get_option(const char* name);
  * is contiguous): head- or batch-sliced views run without a copy (the reference's C ABI assumes
  * contiguous tensors, csrc/paged_attn.cpp:46-60).  strides[12] = {q_batch, q_row, q_head,
  * k_batch, k_row, k_head, v_batch, v_row, v_head, o_batch, o_row, o_head}.  softmax_lse is
- * [batch, num_heads, seqlen_q] contiguous (or NULL).  head_size must be a multiple of 8. */
+ * [batch, num_heads, seqlen_q] contiguous (or NULL).  head_size must be a multiple of 8.
+ * p_dropout / s_dmask: dropout and return_softmax as fmha_fwd (s_dmask = its p_ptr, or NULL). */
 void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, void* softmax_lse,
                       int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
                       int32_t num_heads_k, int32_t head_size, const int64_t* strides,
                       float softmax_scale, int window_size_left, int window_size_right,
-                      float softcap, bool is_fp16, int num_splits, hipStream_t stream);
+                      float softcap, bool is_fp16, int num_splits, hipStream_t stream,
+                      float p_dropout, void* s_dmask);
 
 void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q_scale,
                   float k_scale, float v_scale, int32_t seqlen_q, int32_t seqlen_k,
@@ -131,7 +144,9 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
  * LSE out (fp32 [num_heads, total_q], unpadded as export.cpp:827; total_q = cu_seqlens_q[batch]
  * must be passed by the caller, it is only used to address the LSE), ALiBi, softcap,
  * seqused_k (int32 [batch], optional), and an optional paged K/V (block_table != NULL: k/v are
- * [num_blocks, page, heads_k, head_size], block_table [batch, block_table_stride]). */
+ * [num_blocks, page, heads_k, head_size], block_table [batch, block_table_stride]).
+ * p_dropout / s_dmask: as fmha_fwd (non-paged only; s_dmask [batch, heads,
+ * round128(max_seqlen_q), round128(max_seqlen_k)], each sequence's rows from 0). */
 void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         void* cu_seqlens_q, void* cu_seqlens_k, void* seqused_k,
                         void* block_table, int32_t block_table_stride, int32_t page_block_size,
@@ -139,7 +154,8 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         int32_t max_seqlen_q, int32_t max_seqlen_k, int32_t total_q,
                         int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
                         int32_t head_size, float softmax_scale, int window_size_left,
-                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream);
+                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
+                        float p_dropout, void* s_dmask);
 
 /* Paged-KV forward that also returns LSE (fp32 [batch, num_heads, seqlen_q]) and takes ALiBi
  * and an fp8 (OCP e4m3fn) K/V cache with per-tensor dequant scales.
@@ -186,7 +202,8 @@ void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const
  * 815-1043), which the reference never built.  Inputs dout/q/k/v/out as the fwd layout,
  * softmax_lse fp32 [batch, heads, seqlen_q] from fmha_fwd; outputs dq [b,sq,h,d],
  * dk/dv [b,sk,hk,d] (GQA groups reduced in-kernel, no host sum_out), softmax_d fp32
- * [batch, heads, seqlen_q] (may be NULL: then pool scratch is used).
+ * [batch, heads, seqlen_q] (may be NULL: then pool scratch is used).  p_dropout: the forward's,
+ * with the same fmha_set_rng_state (the keep bits are regenerated, not stored).
  * deterministic: dQ partials of each key block go to their own fp32 slice and are summed in
  * key-block order (bitwise reproducible; export.cpp:1086-1092 splits dq_accum the same way),
  * instead of float atomics into one accumulator.
@@ -207,7 +224,8 @@ size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch
 /* Varlen backward (mha_varlen_bwd semantics, flash_api_hip.cpp:1045-1298): packed q/k/v/out/
  * dout, cu_seqlens int32 [batch+1], softmax_lse fp32 [num_heads, total_q]; softmax_d fp32
  * [num_heads, total_q] receives rowsum(dO*O) (may be NULL: pool scratch).  deterministic and
- * workspace as fmha_bwd (fmha_varlen_bwd_workspace_size(..., deterministic) bytes). */
+ * workspace as fmha_bwd (fmha_varlen_bwd_workspace_size(..., deterministic) bytes); p_dropout as
+ * fmha_bwd. */
 void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
                      void* dq, void* dk, void* dv, void* cu_seqlens_q, void* cu_seqlens_k,
                      void* alibi_slopes, int32_t alibi_batch_stride, int32_t max_seqlen_q,
@@ -216,7 +234,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
                      int32_t head_size, float softmax_scale, int window_size_left,
                      int window_size_right, float softcap, bool deterministic, bool is_fp16,
                      hipStream_t stream, void* workspace, size_t workspace_bytes,
-                     void* softmax_d);
+                     void* softmax_d, float p_dropout);
 
 size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t batch_size,
                                       int32_t num_heads, int32_t num_heads_k, int32_t head_size,

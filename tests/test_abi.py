@@ -71,7 +71,10 @@ def _fwd(**over):
     (dict(h=3, hk=2), "must divide"),
     (dict(d=60), "multiple of 8"),
     (dict(d=512), "at most 256"),
-    (dict(p=0.1), "dropout"),
+    (dict(p=1.0), "p_dropout"),
+    (dict(p=-0.1), "p_dropout"),
+    (dict(ret=True), "return_softmax"),
+    (dict(p=0.1, ret=True), "p and softmax_lse"),
     (dict(sk=0), "positive"),
 ])
 def test_fwd_validation_errors(over, needle):

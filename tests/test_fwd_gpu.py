@@ -351,6 +351,28 @@ def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
     assert (out.float() - ref_gen.float()).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("sq,h,hk", [(1, 32, 8), (3, 12, 1), (2, 64, 2)])
+def test_decode_folded_combine_bitexact(xfa, sq, h, hk):
+    """dec_fold=1 (the last split of each (b, kv head) merges the partials in the decode
+    launch) gives the same output and LSE as the separate combine kernel, bit for bit, twice
+    in a row (the split counters reset themselves)."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(8)
+    b, d, sk = 3, 128, 1500
+    q = torch.randn(b, sq, h, d, dtype=torch.bfloat16).to(DEV)
+    k = torch.randn(b, sk, hk, d, dtype=torch.bfloat16).to(DEV)
+    v = torch.randn(b, sk, hk, d, dtype=torch.bfloat16).to(DEV)
+    base = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    assert L.fmha_set_option(b"dec_fold", 1) == 0
+    try:
+        for _ in range(2):
+            f = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+            assert torch.equal(f[0], base[0]) and torch.equal(f[1], base[1])
+    finally:
+        L.fmha_set_option(b"dec_fold", 0)
+
+
 @pytest.mark.parametrize("window", [(64, 0), (100, 7), (-1, 5)])
 def test_decode_kernel_window_alibi_softcap(xfa, window):
     torch.manual_seed(6)

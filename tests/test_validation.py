@@ -54,7 +54,7 @@ def test_varlen_bwd_slab_guard_dq_accum():
     sq = 1 << 22
     L.fmha_varlen_bwd(FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, None, 0,
                       sq, 128, sq, 128, 1, 1, 1, 128, 0.088, -1, -1, 0.0, False, False, None,
-                      None, 0, None)
+                      None, 0, None, 0.0)
     st, msg = _status()
     assert st != 0 and "dq_accum" in msg
 

@@ -23,11 +23,12 @@ _SIGS = {
     "fmha_page_kvcache_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                               i32, vp, f32, C.c_int, C.c_int, i32, vp, vp, vp, b_, b_, b_],
     "fmha_fwd_strided": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
-                         C.POINTER(C.c_int64), f32, C.c_int, C.c_int, f32, b_, C.c_int, vp],
+                         C.POINTER(C.c_int64), f32, C.c_int, C.c_int, f32, b_, C.c_int, vp,
+                         f32, vp],
     "fmha_fwd_fp8": [vp, vp, vp, vp, vp, f32, f32, f32, i32, i32, i32, i32, i32, i32, f32,
                      C.c_int, C.c_int, b_, vp],
     "fmha_varlen_fwd_ex": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,
-                           i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp],
+                           i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp, f32, vp],
     "fmha_page_kvcache_fwd_ex": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32,
                                  i32, f32, C.c_int, C.c_int, f32, vp, i32, i32, i32, f32, f32, vp,
                                  b_, vp],
@@ -35,7 +36,8 @@ _SIGS = {
                  f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz],
     "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
     "fmha_varlen_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
-                        i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz, vp],
+                        i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz, vp,
+                        f32],
     "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
     "fmha_kvcache_append": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, b_,
                             b_, i32, i32, i32, i32, i32, b_, vp],
@@ -43,6 +45,7 @@ _SIGS = {
     "fmha_last_status": [],
     "fmha_last_num_splits": [],
     "fmha_version": [],
+    "fmha_set_rng_state": [C.c_uint64, C.c_uint64],
     "fmha_set_option": [C.c_char_p, C.c_int],
     "fmha_get_option": [C.c_char_p],
 }

@@ -93,6 +93,23 @@ int* counter_get(hipStream_t st) {
     return c;
 }
 
+// Split-arrival counters of the folded decode combine: >= n ints per (device, stream), zeroed
+// when (re)allocated; every launch leaves them zero (the merging wave resets its counter).
+std::map<std::pair<int, hipStream_t>, std::pair<int*, int>> g_dec_ctr;
+int* dec_counters(hipStream_t st, int n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto& e = g_dec_ctr[{dev, st}];
+    if (e.second >= n) return e.first;
+    if (e.first) { hipStreamSynchronize(st); (void)hipFree(e.first); e.first = nullptr; e.second = 0; }
+    const int want = std::max(n, 1024);
+    if (hipMalloc(&e.first, (size_t)want * 4) != hipSuccess) { e.first = nullptr; return nullptr; }
+    if (hipMemsetAsync(e.first, 0, (size_t)want * 4, st) != hipSuccess) { (void)hipFree(e.first); e.first = nullptr; return nullptr; }
+    e.second = want;
+    return e.first;
+}
+
 // CU count per device (a process may drive several GPUs; cached per device id)
 int num_cus(int dev) {
     static std::mutex mu;
@@ -200,6 +217,30 @@ void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
 }
 
 // Split scratch + launch (shared by every forward entry).
+// Dropout RNG state of the calling thread (fmha_set_rng_state); read by every forward /
+// backward call with p_dropout > 0.
+thread_local uint64_t g_seed = 0, g_offset = 0;
+
+template <typename P>
+bool set_dropout(P& p, float p_dropout) {
+    if (!(p_dropout >= 0.f && p_dropout < 1.f)) return fail(1, "p_dropout must be in [0, 1) (got %g)", p_dropout);
+    p.drop = p_dropout > 0.f;
+    if (!p.drop) return true;
+    const float keep = 1.f - p_dropout;                   // paged_attn.cpp:106-113
+    p.keep_thr = (uint32_t)std::floor(keep * 255.0);
+    p.rp_keep = 1.f / keep;
+    p.seed = g_seed;
+    p.offset = g_offset;
+    return true;
+}
+
+// return_softmax: the dropped-out softmax [b, h, round128(sq), round128(sk)] after the forward
+void run_sdmask(const FwdParams& p, void* s, bool bf16, hipStream_t st) {
+    const int sq_r = (p.seqlen_q + 127) / 128 * 128, sk_r = (p.seqlen_k + 127) / 128 * 128;
+    hip_ok(bf16 ? launch_sdmask_bf16(p, s, sq_r, sk_r, st) : launch_sdmask_f16(p, s, sq_r, sk_r, st),
+           "return_softmax launch");
+}
+
 void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     Options& o = options();
     p.device = current_device();
@@ -213,10 +254,11 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.pipe = o.fwd_pipe.load();
     p.max_slack = (float)o.fwd_slack.load();
     const int n_blocks = (p.seqlen_k + kBlockN - 1) / kBlockN;
+    if (p.drop) num_splits_req = 1;       // no split-KV with dropout (paged_attn.cpp:180)
     int splits = num_splits_req;
     // Decode: the whole GQA group of query rows fits one 32-row MFMA tile -> the split-KV
     // decode kernel (every wave a split, fmha_decode_kernel.h); splits a multiple of 4.
-    p.decode = o.fwd_decode.load() && !p.cu_seqlens_q && !p.cu_seqlens_k &&
+    p.decode = o.fwd_decode.load() && !p.drop && !p.cu_seqlens_q && !p.cu_seqlens_k &&
                p.seqlen_q * p.group <= 32 && hd_bucket(p.d) == p.d && p.d <= 128 &&
                (!p.block_table || p.page_size % 16 == 0);
     if (p.decode) {
@@ -249,6 +291,11 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         p.oaccum = (float*)base;
         p.lseaccum = (float*)(base + (size_t)splits * rows * hd * sizeof(float));
     }
+    p.dec_ctr = nullptr;
+    if (p.decode && o.dec_fold.load()) {
+        p.dec_ctr = dec_counters(st, p.b * p.hk);
+        if (!p.dec_ctr) { fail(3, "could not allocate the decode split counters"); return; }
+    }
     // dynamic item queue: ragged (varlen) row blocks balance across CUs as they finish
     p.work_ctr = nullptr;
     const int dyn = o.fwd_dyn.load();
@@ -268,6 +315,8 @@ int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
 const char* fmha_version(void) { return "xf-fmha-gfx950 2.0"; }
 
+void fmha_set_rng_state(uint64_t seed, uint64_t offset) { g_seed = seed; g_offset = offset; }
+
 int fmha_set_option(const char* name, int value) {
     clear_error();
     if (!name) { fail(1, "option name is null"); return -1; }
@@ -282,6 +331,7 @@ int fmha_set_option(const char* name, int value) {
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 3},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
+        {"dec_fold", &o.dec_fold, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -305,7 +355,7 @@ int fmha_get_option(const char* name) {
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
     XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
-    XFA_GET(bwd_order) XFA_GET(bwd_desc)
+    XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;
@@ -315,15 +365,15 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
               const int32_t seqlen_q, const int32_t seqlen_k, const int32_t batch_size,
               const int32_t num_heads, const int32_t num_heads_k, const int32_t head_size,
               const float p_dropout, hipStream_t stream, hipDeviceProp_t* /*dprops*/,
-              const float softmax_scale, void* /*p_ptr*/, void* softmax_lse_ptr,
+              const float softmax_scale, void* p_ptr, void* softmax_lse_ptr,
               int window_size_left, int window_size_right, const float softcap,
               const bool return_softmax, bool is_fp16, int num_splits) {
     try {
         clear_error();
         if (!check_common(q_ptr, k_ptr, v_ptr, o_ptr, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
-        REQUIRE(p_dropout == 0.f, "dropout is not supported by the forward C path (p_dropout=%g)", p_dropout);
-        REQUIRE(!return_softmax, "return_softmax is only supported with dropout, which this build does not support");
+        REQUIRE(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
+        REQUIRE(!return_softmax || (p_ptr && softmax_lse_ptr), "return_softmax needs the p and softmax_lse buffers");
         if (!slab_ok("q/o", seqlen_q, (int64_t)num_heads * head_size, 2) ||
             !slab_ok("k/v", seqlen_k, (int64_t)num_heads_k * head_size, 2)) return;
         FwdParams p{};
@@ -337,7 +387,9 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes_ptr;
         p.alibi_bstride = batch_size > 1 ? num_heads : 0;   // paged_attn.cpp:375
+        if (!set_dropout(p, p_dropout)) return;
         run_fwd(p, !is_fp16, stream, num_splits);
+        if (return_softmax && g_status == 0) run_sdmask(p, p_ptr, !is_fp16, stream);
     } catch (...) {
         fail(9, "internal error in fmha_fwd");
     }
@@ -347,7 +399,8 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
                       int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size, int32_t num_heads,
                       int32_t num_heads_k, int32_t head_size, const int64_t* st,
                       float softmax_scale, int window_size_left, int window_size_right,
-                      float softcap, bool is_fp16, int num_splits, hipStream_t stream) {
+                      float softcap, bool is_fp16, int num_splits, hipStream_t stream,
+                      float p_dropout, void* s_dmask) {
     try {
         clear_error();
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
@@ -379,7 +432,10 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes;
         p.alibi_bstride = batch_size > 1 ? num_heads : 0;
+        REQUIRE(!s_dmask || (p_dropout > 0.f && softmax_lse), "s_dmask needs p_dropout > 0 and softmax_lse");
+        if (!set_dropout(p, p_dropout)) return;
         run_fwd(p, !is_fp16, stream, num_splits);
+        if (s_dmask && g_status == 0) run_sdmask(p, s_dmask, !is_fp16, stream);
     } catch (...) {
         fail(9, "internal error in fmha_fwd_strided");
     }
@@ -431,7 +487,8 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         int32_t max_seqlen_q, int32_t max_seqlen_k, int32_t total_q,
                         int32_t batch_size, int32_t num_heads, int32_t num_heads_k,
                         int32_t head_size, float softmax_scale, int window_size_left,
-                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream) {
+                        int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
+                        float p_dropout, void* s_dmask) {
     try {
         clear_error();
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
@@ -473,7 +530,12 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
         p.lse_batch = 0;
         p.lse_head = total_q;
         REQUIRE(!softmax_lse || total_q > 0, "total_q must be given to address the LSE");
+        REQUIRE(!s_dmask || (p_dropout > 0.f && softmax_lse && !block_table),
+                "s_dmask needs p_dropout > 0, softmax_lse and a non-paged K/V");
+        REQUIRE(p_dropout == 0.f || !block_table, "dropout over a paged K/V cache is not supported");
+        if (!set_dropout(p, p_dropout)) return;
         run_fwd(p, !is_fp16, stream, 1);
+        if (s_dmask && g_status == 0) run_sdmask(p, s_dmask, !is_fp16, stream);
     } catch (...) {
         fail(9, "internal error in fmha_varlen_fwd_ex");
     }
@@ -489,7 +551,8 @@ void fmha_varlen_fwd(void* q_ptrs, void* k_ptrs, void* v_ptrs, void* o_ptrs,
     fmha_varlen_fwd_ex(q_ptrs, k_ptrs, v_ptrs, o_ptrs, nullptr, cu_seqlens_q_ptrs,
                        cu_seqlens_k_ptrs, nullptr, nullptr, 0, 0, nullptr, 0, max_seqlen_q,
                        max_seqlen_k, 0, batch_size, num_heads, num_heads_k, head_size,
-                       softmax_scale, window_size_left, window_size_right, 0.f, is_fp16, stream);
+                       softmax_scale, window_size_left, window_size_right, 0.f, is_fp16, stream,
+                       0.f, nullptr);
 }
 
 void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
@@ -675,7 +738,6 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
-        REQUIRE(p_dropout == 0.f, "dropout is not supported by the backward (p_dropout=%g)", p_dropout);
         const int h = num_heads, hk = num_heads_k, d = head_size;
         if (!slab_ok("q/out/dout/dq", seqlen_q, (int64_t)h * d, 2) ||
             !slab_ok("k/v/dk/dv", seqlen_k, (int64_t)hk * d, 2) ||
@@ -715,6 +777,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, seqlen_k);
+        if (!set_dropout(p, p_dropout)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_bwd");
@@ -729,7 +792,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
                      int32_t head_size, float softmax_scale, int window_size_left,
                      int window_size_right, float softcap, bool deterministic, bool is_fp16,
                      hipStream_t stream, void* workspace, size_t workspace_bytes,
-                     void* softmax_d) {
+                     void* softmax_d, float p_dropout) {
     try {
         clear_error();
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
@@ -779,6 +842,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, max_seqlen_k);
+        if (!set_dropout(p, p_dropout)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "varlen backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_varlen_bwd");

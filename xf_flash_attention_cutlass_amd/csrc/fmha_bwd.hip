@@ -27,7 +27,7 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
     if (e != hipSuccess) return e;
 
     const bool mask = p.wl >= 0 || p.wr >= 0;
-    const bool feat = p.alibi || p.softcap_on || p.cu_seqlens_q || p.cu_seqlens_k;
+    const bool feat = p.alibi || p.softcap_on || p.cu_seqlens_q || p.cu_seqlens_k || p.drop;
     void (*kern)(const BwdParams) =
         p.dq_slices ? fmha_bwd_kernel<HD, T, true, true, true>
         : mask ? (feat ? fmha_bwd_kernel<HD, T, true, true> : fmha_bwd_kernel<HD, T, true, false>)

@@ -474,25 +474,36 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 }
             }
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
+            for (int ks = 0; ks < KS; ++ks) {
+                // dropout: the 4 rows pos0 .. +3 of this lane's key are one Philox block
+                // (fmha_common.h drop_block, the forward's draw); kept P scaled by 1 / p_keep
+                u32x4 dw = u32x4{0, 0, 0, 0};
+                if (FEAT && p.drop) dw = drop_block(p.seed, p.offset, bidx * p.h + head, pos0, my_key[ks]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = 4 * gq + i;
-                const int pos = pos0 + i;
-                const int key = my_key[ks];
-                float w = s_acc[ks][r];
-                float dcap = 1.f;
-                if (FEAT && p.softcap_on) { w = fast_tanh(w * p.softcap_pre); dcap = 1.f - w * w; }
-                if (FEAT && p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
-                float pr = fast_exp2(fmaf(w, c, -lse4[i]));
-                if (need_mask) {
-                    // visible keys of row pos: [lo, hi) -> one unsigned compare
-                    const int hi = (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk;
-                    const int lo = (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0;
-                    pr = (unsigned)(key - lo) < (unsigned)max(hi - lo, 0) ? pr : 0.f;
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 4 * gq + i;
+                    const int pos = pos0 + i;
+                    const int key = my_key[ks];
+                    float w = s_acc[ks][r];
+                    float dcap = 1.f;
+                    if (FEAT && p.softcap_on) { w = fast_tanh(w * p.softcap_pre); dcap = 1.f - w * w; }
+                    if (FEAT && p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
+                    float pr = fast_exp2(fmaf(w, c, -lse4[i]));
+                    if (need_mask) {
+                        // visible keys of row pos: [lo, hi) -> one unsigned compare
+                        const int hi = (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk;
+                        const int lo = (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0;
+                        pr = (unsigned)(key - lo) < (unsigned)max(hi - lo, 0) ? pr : 0.f;
+                    }
+                    if (FEAT && p.drop) {
+                        const bool keep = drop_keep(dw[i], key & 3, p.keep_thr);
+                        s_acc[ks][r] = keep ? pr * p.rp_keep : 0.f;
+                        dp_acc[ks][r] = pr * ((keep ? dp_acc[ks][r] * p.rp_keep : 0.f) - d4[i]) * dcap;
+                    } else {
+                        s_acc[ks][r] = pr;
+                        dp_acc[ks][r] = pr * (dp_acc[ks][r] - d4[i]) * dcap;
+                    }
                 }
-                s_acc[ks][r] = pr;
-                dp_acc[ks][r] = pr * (dp_acc[ks][r] - d4[i]) * dcap;
             }
         }
         // ---- dV^T += dO^T P ; dK^T += Q^T dS  (P / dS accumulators are the B operands)

@@ -119,6 +119,8 @@ struct FwdParams {
     int dec_mr;                // decode: 16 -> the 16x16x32 tile (query rows <= 16)
     int dec_hmaj;              // decode: the 4 waves of a workgroup are 4 kv heads of one split
     int* work_ctr;             // persistent == 3: self-resetting counters [-, finished, next x 8]
+    int* dec_ctr;              // decode, combine folded in: per (batch, kv head) split arrival
+                               // counters (zero between launches: the merging wave resets its own)
     int xcd_queues;            // persistent == 3: one item queue per XCD (else queue 0 only)
     // host-side launch choices (snapshotted from the options by the C ABI, per call)
     int waves;                 // 4 or 8 waves per workgroup (D <= 128)
@@ -128,6 +130,13 @@ struct FwdParams {
     int xcdq;                  // dynamic queue kind (1 per-XCD queues)
     int device;                // current device id (per-device one-time kernel attributes)
     int fwd4;                  // 1: the 4-wave D = 128 forward where eligible (fmha_fwd4_kernel.h)
+    // dropout (flash_fwd_kernel_hip.h's Dropout, dropout_hip.h:14-109): keep a score iff its
+    // Philox byte <= keep_thr (= floor(p_keep * 255), paged_attn.cpp:106-113); kept P scaled by
+    // rp_keep = 1 / p_keep.  drop = 0: no dropout.
+    int drop;
+    uint32_t keep_thr;
+    float rp_keep;
+    uint64_t seed, offset;
 };
 
 struct CombineParams {
@@ -176,7 +185,45 @@ struct BwdParams {
     int device;          // current device id (per-device one-time kernel attributes)
     int order;           // 1: 1-D grid, the key blocks of one (batch, kv head) consecutive on one XCD
     int desc;            // 1: each key block sweeps its query tiles last to first
+    // dropout (flash_fwd_kernel_hip.h's Dropout, dropout_hip.h:14-109): keep a score iff its
+    // Philox byte <= keep_thr (= floor(p_keep * 255), paged_attn.cpp:106-113); kept P scaled by
+    // rp_keep = 1 / p_keep.  drop = 0: no dropout.
+    int drop;
+    uint32_t keep_thr;
+    float rp_keep;
+    uint64_t seed, offset;
 };
+
+// ------------------------------------------------------------------ dropout RNG --
+// Philox4x32 with 7 rounds: the reference's philox() (philox.cuh:32-50, six rounds plus the
+// final one, Weyl key bumps), here on a counter of the score's coordinates.
+__device__ __forceinline__ u32x4 philox4x32_7(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
+                                              uint32_t c2, uint32_t c3) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return u32x4{c0, c1, c2, c3};
+}
+// The random bytes of one 4 x 4 block of scores of (batch, head) bh = b * H + h: query positions
+// 4 (pos >> 2) .. +3, keys 4 (key >> 2) .. +3.  Word i is query position 4 (pos >> 2) + i, its
+// byte j key 4 (key >> 2) + j.  (A forward lane holds one query row and runs of 4 keys, a
+// backward lane one key and runs of 4 query rows: both draw one block per run.)
+// Keep a score iff its byte <= keep_thr.  Restated on the CPU by oracle/dropout_ref.py.
+__device__ __forceinline__ u32x4 drop_block(const uint64_t seed, const uint64_t offset, const int bh,
+                                            const int pos, const int key) {
+    return philox4x32_7((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32),
+                        (uint32_t)key >> 2, (uint32_t)pos >> 2, (uint32_t)bh, (uint32_t)offset);
+}
+__device__ __forceinline__ bool drop_keep(const uint32_t word, const int j, const uint32_t thr) {
+    return ((word >> (8 * j)) & 0xFFu) <= thr;
+}
 
 // ------------------------------------------------------------------ dtype traits --
 template <typename T> struct DT;

@@ -394,19 +394,122 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
     const float l_full = MR == 32 ? wave_sum_halves(l_run) : quad_sum16(l_run);
     const bool empty = (l_full == 0.f) || (l_full != l_full);
     const float inv = empty ? 0.f : (KV8 ? p.v_scale : 1.f) / l_full;
-    if (!row_ok) return;
-    const int64_t rid = (((int64_t)split * p.b + bidx) * p.h + head) * sq + pos;
-    float* oa = p.oaccum + rid * HD;
+    if (row_ok) {
+        const int64_t rid = (((int64_t)split * p.b + bidx) * p.h + head) * sq + pos;
+        float* oa = p.oaccum + rid * HD;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+        for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-        for (int g = 0; g < NA / 4; ++g) {
-            // O^T element (dt, 4g + v): d = 32 dt + 8 g + 4 hh + v (MR 32), 16 dt + 4 hh + v (MR 16)
-            const int d = MR == 32 ? 32 * dt + 8 * g + 4 * hh : 16 * dt + 4 * hh;
-            *reinterpret_cast<f32x4*>(oa + d) = f32x4{acc_o[dt][4 * g] * inv, acc_o[dt][4 * g + 1] * inv,
-                                                      acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv};
+            for (int g = 0; g < NA / 4; ++g) {
+                // O^T element (dt, 4g + v): d = 32 dt + 8 g + 4 hh + v (MR 32), 16 dt + 4 hh + v (MR 16)
+                const int d = MR == 32 ? 32 * dt + 8 * g + 4 * hh : 16 * dt + 4 * hh;
+                const f32x4 v = f32x4{acc_o[dt][4 * g] * inv, acc_o[dt][4 * g + 1] * inv,
+                                      acc_o[dt][4 * g + 2] * inv, acc_o[dt][4 * g + 3] * inv};
+                if (p.dec_ctr) {
+                    // folded combine: device-coherent stores (sc1, through to memory; the
+                    // merging wave may sit on another XCD, whose L2 is not this one's)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        __hip_atomic_store(oa + d + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    *reinterpret_cast<f32x4*>(oa + d) = v;
+                }
+            }
+        const float lsev = empty ? -INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+        if (hh == 0) {
+            if (p.dec_ctr) __hip_atomic_store(p.lseaccum + rid, lsev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else p.lseaccum[rid] = lsev;
         }
-    if (hh == 0) p.lseaccum[rid] = empty ? -INFINITY : (m_run * c + __log2f(l_full)) * kLn2;
+    }
+    if (!p.dec_ctr) return;
+
+    // ---- folded combine: the last of the (b, kv head)'s splits to arrive merges its rows
+    // (the reference's combine_attn_seqk_parallel, flash_fwd_kernel_hip.h:1322-1568).  The
+    // partials went out as device-coherent stores; once they are complete (vmcnt counts
+    // stores) the arrival is counted; the merging wave reads them with device-coherent loads.
+    // No L2 write-back / invalidate fences (one per wave cost ~100 us on C5).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* ctr = p.dec_ctr + bidx * p.hk + hk_i;
+    int old = 0;
+    if (lane == 0) old = atomicAdd(ctr, 1);
+    old = __builtin_amdgcn_readfirstlane(__shfl(old, 0));
+    if (old != p.num_splits - 1) return;
+    const int ns = p.num_splits;                 // <= 128 (host)
+    const int64_t nrows = (int64_t)p.b * p.h * sq;
+    auto rid_of = [&](int r) {
+        const int rpos = r / G;
+        return ((int64_t)bidx * p.h + hk_i * G + (r - rpos * G)) * sq + rpos;
+    };
+    // phase 1, per row: merged LSE over the splits (lanes over splits, every row's loads in
+    // flight together) and each split's weight exp(lse_s - lse) -> this wave's LDS slice
+    float* wbuf = reinterpret_cast<float*>(vsl);  // [row][split], 32 x 128 floats <= 2 SLICE
+    constexpr int RC = MR == 32 ? 4 : 8;         // rows per chunk (bounds the registers)
+    for (int r0 = 0; r0 < rows; r0 += RC) {
+        float ls0[RC], ls1[RC];
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            ls0[u] = ls1[u] = -INFINITY;
+            if (r0 + u < rows) {
+                const int64_t rid = rid_of(r0 + u);
+                if (lane < ns) ls0[u] = __hip_atomic_load(p.lseaccum + lane * nrows + rid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane + 64 < ns) ls1[u] = __hip_atomic_load(p.lseaccum + (lane + 64) * nrows + rid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RC; ++u) {
+            const int r = r0 + u;
+            if (r >= rows) break;
+            float mx = wave_max_halves(fmaxf(ls0[u], ls1[u]));
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+            float sum = mx == -INFINITY ? 0.f : __expf(ls0[u] - mx) + __expf(ls1[u] - mx);
+            sum = wave_sum_halves(sum);
+#pragma unroll
+            for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+            const bool rempty = (mx == -INFINITY) || sum == 0.f;
+            const float lse = rempty ? INFINITY : __logf(sum) + mx;
+            if (lane < ns) wbuf[r * ns + lane] = rempty ? 0.f : __expf(ls0[u] - lse);
+            if (lane + 64 < ns) wbuf[r * ns + lane + 64] = rempty ? 0.f : __expf(ls1[u] - lse);
+            if (p.lse && lane == 0) {
+                const int rpos = r / G;
+                p.lse[(int64_t)bidx * p.lse_batch + (int64_t)(hk_i * G + r - rpos * G) * p.lse_head + rpos] = lse;
+            }
+        }
+    }
+    // phase 2: O = sum_s w_s O_s; lane -> 4 d values (lane & 31) of rows r0 + 2 rr + (lane >> 5)
+    const int d4 = (lane & 31) * 4;
+    const int hr = lane >> 5;
+    for (int r0 = 0; r0 < rows; r0 += RC) {
+        f32x4 acc[RC / 2];
+#pragma unroll
+        for (int rr = 0; rr < RC / 2; ++rr) acc[rr] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < ns; ++sp) {
+            const float* os = p.oaccum + (int64_t)sp * nrows * HD;
+#pragma unroll
+            for (int rr = 0; rr < RC / 2; ++rr) {
+                const int r = r0 + 2 * rr + hr;
+                if (r < rows && d4 < HD) {
+                    const float* src = os + rid_of(r) * HD + d4;
+                    f32x4 x;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    acc[rr] += wbuf[r * ns + sp] * x;
+                }
+            }
+        }
+#pragma unroll
+        for (int rr = 0; rr < RC / 2; ++rr) {
+            const int r = r0 + 2 * rr + hr;
+            if (r >= rows) continue;
+            const int rpos = r / G;
+            T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch + (int64_t)rpos * p.o_row +
+                      (int64_t)(hk_i * G + r - rpos * G) * p.o_head;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (d4 + i < p.d) orow[d4 + i] = (T)acc[rr][i];
+        }
+    }
+    if (lane == 0) atomicExch(ctr, 0);
 }
 
 }  // namespace xfa

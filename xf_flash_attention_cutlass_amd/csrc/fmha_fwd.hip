@@ -7,6 +7,7 @@
 #include "fmha_fwd4_kernel.h"
 #endif
 #include "fmha_decode_kernel.h"
+#include "fmha_sdmask_kernel.h"
 #include "fmha_launch.h"
 
 #ifndef XFA_HD
@@ -76,6 +77,7 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (p.dec_ctr) return hipSuccess;          // the last split of each (b, kv head) merged
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
 }
 
@@ -83,7 +85,7 @@ template <int HD, typename T, int NW>
 static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     const bool mask = p.wl >= 0 || p.wr >= 0;
     // FEAT: per-score transforms (ALiBi, softcap) and the paged / fp8 staging paths
-    const bool feat = p.alibi || p.softcap_pre > 0.f || p.block_table || p.kv_fp8;
+    const bool feat = p.alibi || p.softcap_pre > 0.f || p.block_table || p.kv_fp8 || p.drop;
     const int rows = p.seqlen_q * p.group;
     const int n_mb = (rows + NW * 32 - 1) / (NW * 32);
     dim3 grid(p.b * p.hk, n_mb, p.num_splits > 1 ? p.num_splits : 1);
@@ -122,7 +124,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 static bool fwd4_eligible(const FwdParams& p) {
     return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 &&
            (p.wl < 0 || p.wl >= p.seqlen_k) && !p.alibi &&
-           !(p.softcap_pre > 0.f) && !p.block_table && !p.kv_fp8 && !p.leftpad_k;
+           !(p.softcap_pre > 0.f) && !p.block_table && !p.kv_fp8 && !p.leftpad_k && !p.drop;
 }
 
 static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
@@ -152,6 +154,16 @@ extern "C" void XFA_CAT(fmha_fwd4_stamp_, XFA_DTN)(unsigned long long* out) {
     (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd4_stamp), 4 * sizeof(unsigned long long));
     const unsigned long long z[4] = {0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_stamp), z, sizeof(z));
+}
+#endif
+
+#if XFA_HD == 128
+// return_softmax with dropout (fmha_sdmask_kernel.h): s [b, h, sq_r, sk_r] in the q dtype
+hipError_t XFA_CAT(launch_sdmask_, XFA_DTN)(const FwdParams& p, void* s, int sq_r, int sk_r, hipStream_t st) {
+    const int64_t s_head = (int64_t)sq_r * sk_r;
+    hipLaunchKernelGGL((fmha_sdmask_kernel<elem_t>), dim3(p.b * p.h, sq_r), dim3(256), 0, st, p,
+                       reinterpret_cast<elem_t*>(s), s_head * p.h, s_head, sk_r);
+    return hipGetLastError();
 }
 #endif
 

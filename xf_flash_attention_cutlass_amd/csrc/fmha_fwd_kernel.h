@@ -293,6 +293,23 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
             pb[2 * kt + (r >> 3)][(r & 7) + 1] = e[1];
         }
     };
+    // dropout on the P operand of PV (the row sums keep the undropped P, as the reference's
+    // softmax does before apply_dropout, flash_fwd_kernel_hip.h): each run of 4 keys of this
+    // lane's row draws one Philox block (fmha_common.h drop_block)
+    auto drop_tile = [&](V8 (&pb)[4], const int n0) {
+        if (!(FEAT && p.drop)) return;
+        const int bhg = bidx * p.h + head;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 w = drop_block(p.seed, p.offset, bhg, pos, n0 + 32 * kt + 8 * j + 4 * hh);
+                const uint32_t word = (pos & 2) ? ((pos & 1) ? w[3] : w[2]) : ((pos & 1) ? w[1] : w[0]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (!drop_keep(word, i, p.keep_thr)) pb[2 * kt + (j >> 1)][(j & 1) * 4 + i] = (T)0.f;
+            }
+    };
     auto exp_ref = [&]() {
         const float mref = (m_sc == -INFINITY) ? 0.f : m_sc;
         return f2{mref, mref};
@@ -394,6 +411,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 raise_max(row_max(st));
                 V8 pb[4];
                 exp_tile(st, pb);
+                drop_tile(pb, n0);
                 pv(buf, pb);
             }
             if (more) store_from(buf ^ 1, kr, vr);
@@ -487,6 +505,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
                 raise_max(row_max(st));
                 V8 pb[4];
                 exp_tile(st, pb);
+                drop_tile(pb, n0);
                 pv(buf, pb);
             }
             publish(false);
@@ -676,7 +695,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     // [f_lo, f_hi) every row of the workgroup sees in full; [f_hi, nb_hi) cross the right
     // window edge / the end of the keys.  The last two ranges run through the pipeline.
     int f_lo = nb_hi, f_hi = nb_hi;
-    if (PIPE && p.pipe && !paged && !kv8) {
+    if (PIPE && p.pipe && !paged && !kv8 && !(FEAT && p.drop)) {
         const int ll_max = lim_l(pos_hi), lr_min = lim_r(pos_lo);
         f_lo = max(nb_lo, (ll_max + kBlockN - 1) / kBlockN);
         f_hi = max(f_lo, min(nb_hi, lr_min / kBlockN));
@@ -714,7 +733,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     }
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)bidx * p.o_batch +
               (int64_t)(q_off + pos) * p.o_row + (int64_t)head * p.o_head;
-    store_o_row16<T, ND>(orow, acc_o, inv, p.d, hh);
+    store_o_row16<T, ND>(orow, acc_o, (FEAT && p.drop) ? inv * p.rp_keep : inv, p.d, hh);
     if (p.lse && hh == 0) {
         p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] =
             empty ? INFINITY : (m_sc + __log2f(l_full)) * kLn2;

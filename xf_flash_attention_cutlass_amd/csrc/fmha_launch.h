@@ -28,6 +28,10 @@ struct Options {
     std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
     std::atomic<int> dec_mr{16};         // decode MFMA rows: 16 when the query rows fit 16 (C5: 105 vs
                                          // 110 us with dec_hmaj = 1), else 32
+    std::atomic<int> dec_fold{0};        // decode: the last split of each (b, kv head) merges the partials
+                                         // (no separate combine launch; C5: 126.8 vs 105.5 us - the
+                                         // coherent partial stores and the 64-wave merge tail cost
+                                         // more than the 5 us combine launch they replace)
     std::atomic<int> bwd_order{0};       // backward grid: 1 = the key blocks of one (b, kv head) consecutive
                                          // on one XCD (they then sweep the same Q / dO tiles together;
                                          // C3: 3.03 vs 2.88 ms - their dQ atomics then collide)
@@ -57,6 +61,9 @@ hipError_t launch_bwd_hd256_f16(const BwdParams& p, hipStream_t st);
 
 // fp8 (e4m3fn) Q/K/V forward, D = 128 (fmha_fwd_fp8.hip): bf16 or fp16 output.
 hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st);
+// return_softmax with dropout: the dropped-out softmax [b, h, sq_r, sk_r] (fmha_sdmask_kernel.h)
+hipError_t launch_sdmask_bf16(const FwdParams& p, void* s, int sq_r, int sk_r, hipStream_t st);
+hipError_t launch_sdmask_f16(const FwdParams& p, void* s, int sq_r, int sk_r, hipStream_t st);
 
 // KV-cache append (+ rotary) pass, fmha_append.hip
 struct AppendParams {

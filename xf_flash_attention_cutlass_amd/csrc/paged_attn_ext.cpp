@@ -11,10 +11,12 @@
 // as RuntimeError.  Behaviour the reference gets wrong is fixed, not copied:
 // LSE is always written; GQA decode is handled by the kernel's head packing instead of the
 // transposed-view swap (:526-532); a [H]-shaped ALiBi vector is expanded rather than read
-// out of bounds; dropout is rejected instead of silently ignored.
+// out of bounds; dropout runs (Philox keep bits, rng_state = {seed, offset} as export.cpp
+// returns it) instead of being silently ignored.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/HIPGeneratorImpl.h>
 
 #include <limits>
 
@@ -67,13 +69,43 @@ at::Tensor alibi_for_c(c10::optional<at::Tensor>& a, int b, int h, int64_t* bstr
     return s;
 }
 
+// Dropout: seed / offset from torch's HIP generator (flash-attn's philox_cuda_state use,
+// export.cpp:616-627), handed to the C ABI's thread RNG state; returned as rng_state
+// (int64 [2] on the host: the backward reads it without a device round trip).
+at::Tensor dropout_rng(float p_dropout, c10::optional<at::Generator>& gen_, int64_t counter_offset) {
+    uint64_t seed = 0, offset = 0;
+    if (p_dropout > 0.f) {
+        auto gen = at::get_generator_or_default<at::CUDAGeneratorImpl>(gen_, at::cuda::detail::getDefaultCUDAGenerator());
+        std::lock_guard<std::mutex> lock(gen->mutex_);
+        auto so = gen->philox_engine_inputs((uint64_t)counter_offset);
+        seed = so.first;
+        offset = so.second;
+    }
+    fmha_set_rng_state(seed, offset);
+    return torch::tensor({(int64_t)seed, (int64_t)offset}, torch::dtype(torch::kInt64));
+}
+
+void dropout_rng_restore(float p_dropout, c10::optional<at::Tensor>& rng_state) {
+    if (p_dropout <= 0.f) return;
+    TORCH_CHECK(rng_state.has_value(), "backward with dropout needs the forward's rng_state");
+    auto r = rng_state.value().to(torch::kCPU).to(torch::kInt64).contiguous();
+    TORCH_CHECK(r.numel() == 2, "rng_state must hold {seed, offset}");
+    fmha_set_rng_state((uint64_t)r.data_ptr<int64_t>()[0], (uint64_t)r.data_ptr<int64_t>()[1]);
+}
+
+at::Tensor sdmask_buffer(bool want, const at::TensorOptions& opts, int b, int h, int sq, int sk) {
+    if (!want) return at::Tensor();
+    auto r128 = [](int x) { return (x + 127) / 128 * 128; };
+    return torch::empty({b, h, r128(sq), r128(sk)}, opts);
+}
+
 }  // namespace
 
 std::vector<at::Tensor>
 mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<at::Tensor>& out_,
         c10::optional<at::Tensor>& alibi_slopes_, const float p_dropout, const float softmax_scale,
         bool is_causal, int window_size_left, int window_size_right, const float softcap,
-        const bool return_softmax, c10::optional<at::Generator> /*gen_*/) {
+        const bool return_softmax, c10::optional<at::Generator> gen_) {
     check_qkv_dtype(q, k, v);
     const auto sizes = q.sizes();
     TORCH_CHECK(q.dim() == 4, "q must be (batch, seqlen, heads, head_size)");
@@ -86,8 +118,8 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     TORCH_CHECK(batch_size > 0, "batch size must be postive");
     TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
-    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
-    TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
+    TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    TORCH_CHECK(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
     if (window_size_left >= seqlen_k) window_size_left = -1;
     if (window_size_right >= seqlen_k) window_size_right = -1;
     if (seqlen_q == 1 && !alibi_slopes_.has_value()) is_causal = false;
@@ -117,8 +149,8 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
     auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
-    at::Tensor p;
-    auto rng_state = torch::empty({2}, opts.dtype(torch::kInt64));
+    at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, seqlen_q, seqlen_k);
+    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32);
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
 
@@ -130,14 +162,15 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
                          alibi.defined() ? alibi.data_ptr() : nullptr, softmax_lse.data_ptr(),
                          seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k, head_size, st,
                          softmax_scale, window_size_left, window_size_right, softcap,
-                         q.dtype() == torch::kFloat16, 0, cur_stream());
+                         q.dtype() == torch::kFloat16, 0, cur_stream(), p_dropout,
+                         p.defined() ? p.data_ptr() : nullptr);
         raise_if_failed("fwd");
     } else if (seqlen_k > 0) {
         fmha_fwd(q_padded.data_ptr(), k_padded.data_ptr(), v_padded.data_ptr(), out.data_ptr(),
                  alibi.defined() ? alibi.data_ptr() : nullptr, seqlen_q, seqlen_k, batch_size,
                  num_heads, num_heads_k, head_size, p_dropout, cur_stream(), nullptr, softmax_scale,
-                 nullptr, softmax_lse.data_ptr(), window_size_left, window_size_right, softcap,
-                 return_softmax, q.dtype() == torch::kFloat16, 0);
+                 p.defined() ? p.data_ptr() : nullptr, softmax_lse.data_ptr(), window_size_left,
+                 window_size_right, softcap, return_softmax, q.dtype() == torch::kFloat16, 0);
         raise_if_failed("fwd");
     } else {
         out.zero_();
@@ -157,7 +190,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                int max_seqlen_q, const int max_seqlen_k, const float p_dropout,
                const float softmax_scale, const bool zero_tensors, bool is_causal,
                int window_size_left, int window_size_right, const float softcap,
-               const bool return_softmax, c10::optional<at::Generator> /*gen_*/) {
+               const bool return_softmax, c10::optional<at::Generator> gen_) {
     check_qkv_dtype(q, k, v);
     TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
     TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
@@ -180,8 +213,9 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     TORCH_CHECK(batch_size > 0, "batch size must be positive");
     TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
-    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
-    TORCH_CHECK(!return_softmax, "return_softmax is only supported when p_dropout > 0.0");
+    TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    TORCH_CHECK(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
+    TORCH_CHECK(p_dropout == 0.f || !paged_KV, "dropout over a paged K/V cache is not supported");
     const int max_num_blocks_per_seq = !paged_KV ? 0 : block_table.size(1);
     const int num_blocks = !paged_KV ? 0 : k.size(0);
     const int page_block_size = !paged_KV ? 1 : k.size(1);
@@ -227,8 +261,8 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
     auto softmax_lse = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
-    at::Tensor p;
-    auto rng_state = torch::empty({2}, opts.dtype(torch::kInt64));
+    at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, max_seqlen_q, max_seqlen_k);
+    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32);
     if (zero_tensors) {
         out.zero_();
         softmax_lse.fill_(-std::numeric_limits<float>::infinity());
@@ -244,7 +278,8 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                            alibi.defined() ? alibi.data_ptr() : nullptr, (int)alibi_bs,
                            max_seqlen_q, max_seqlen_k, total_q, batch_size, num_heads, num_heads_k,
                            head_size, softmax_scale, window_size_left, window_size_right, softcap,
-                           q.dtype() == torch::kFloat16, cur_stream());
+                           q.dtype() == torch::kFloat16, cur_stream(), p_dropout,
+                           p.defined() ? p.data_ptr() : nullptr);
         raise_if_failed("varlen_fwd");
     } else {
         out.zero_();
@@ -451,13 +486,14 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
         c10::optional<at::Tensor>& alibi_slopes_, const float p_dropout,
         const float softmax_scale, const bool is_causal, int window_size_left,
         int window_size_right, const float softcap, const bool deterministic,
-        c10::optional<at::Generator> /*gen_*/, c10::optional<at::Tensor>& /*rng_state*/) {
+        c10::optional<at::Generator> /*gen_*/, c10::optional<at::Tensor>& rng_state) {
     check_qkv_dtype(q, k, v);
     if (is_causal) window_size_right = 0;
     TORCH_CHECK(out.dtype() == q.dtype(), "query and out must have the same dtype");
     TORCH_CHECK(dout.dtype() == q.dtype(), "query and dout must have the same dtype");
     CHECK_DEVICE(out); CHECK_DEVICE(dout); CHECK_DEVICE(softmax_lse);
-    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    dropout_rng_restore(p_dropout, rng_state);
     const auto sizes = q.sizes();
     const int batch_size = sizes[0];
     const int seqlen_q = sizes[1];
@@ -522,10 +558,11 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
                const float softmax_scale, const bool zero_tensors, const bool is_causal,
                int window_size_left, int window_size_right, const float softcap,
                const bool deterministic, c10::optional<at::Generator> /*gen_*/,
-               c10::optional<at::Tensor>& /*rng_state*/) {
+               c10::optional<at::Tensor>& rng_state) {
     check_qkv_dtype(q, k, v);
     if (is_causal) window_size_right = 0;
-    TORCH_CHECK(p_dropout == 0.f, "dropout is not supported by this build");
+    TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    dropout_rng_restore(p_dropout, rng_state);
     TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
     TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
     const int batch_size = cu_seqlens_q.numel() - 1;
@@ -561,7 +598,7 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
                     max_seqlen_k, total_q, total_k, batch_size, num_heads, num_heads_k, head_size,
                     softmax_scale, window_size_left, window_size_right, softcap, deterministic,
                     q.dtype() == torch::kFloat16, cur_stream(), workspace.data_ptr(), ws,
-                    softmax_d.data_ptr());
+                    softmax_d.data_ptr(), p_dropout);
     raise_if_failed("varlen_bwd");
     (void)zero_tensors;
     grad_writeback(dq_, dq); grad_writeback(dk_, dk); grad_writeback(dv_, dv);
