@@ -422,7 +422,7 @@ def build_workload(a, mode, dev, rank, world):
 
 def measured_traffic(mode):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (profiles/r*_traffic.json, written by tools/traffic.py from rocprofv3 --pmc passes with
+    (profiles/r*_traffic.json, written by tools/pmc_report.py from rocprofv3 --pmc passes with
     the gfx950 FETCH_SIZE x2 correction), or None."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
     if not files:
@@ -497,7 +497,8 @@ def sub_result(a, mode, dev, stream, **over):
     u = 1e9 if hbm else 1e12
     out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
            "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
-           "unit": "GB/s" if hbm else "TFLOP/s", "roofline": roofline(w, ev, mode)}
+           "unit": "GB/s" if hbm else "TFLOP/s",
+           "roofline": roofline(w, ev, mode + ("_ragged" if a.ragged else ""))}
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = w["cpu"]()
     del w
@@ -686,7 +687,7 @@ def main(argv=None):
             "options": dict(o.split("=") for o in a.opt),
             "library": capi.lib().fmha_version().decode(),
             "config": w["config"],
-            "roofline": roofline(w, ev_ms, a.mode),
+            "roofline": roofline(w, ev_ms, a.mode + ("_ragged" if a.ragged else "")),
         }
         if dist:
             line["rccl"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}

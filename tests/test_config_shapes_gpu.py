@@ -136,10 +136,12 @@ def test_c4_full_shape(xfa, parity_report):
     assert torch.equal(out, out_static)
 
 
-def test_c5_full_shape(xfa, parity_report):
+@pytest.mark.parametrize("ragged", [False, True])
+def test_c5_full_shape(xfa, parity_report, ragged):
     """The benched decode shape and path: B8 H32 Hk8, 32768 cached tokens per sequence, page 16,
     fp8 e4m3fn K/V (scales 1/16), random-permutation block table; the split heuristic picks the
-    32-split decode launch (checked).  Every sequence is compared with the oracle over the
+    32-split decode launch (checked).  ragged: the cache lengths of `bench.py --ragged`
+    (U[1, 32768], the same generator seed).  Every sequence is compared with the oracle over the
     dequantised cache (kvcache rule, test.py:1593-1594)."""
     B, S, H, HK, D, page = 8, 32768, 32, 8, 128, 16
     nblk = S // page
@@ -150,7 +152,11 @@ def test_c5_full_shape(xfa, parity_report):
     kc8 = (_rand((nblocks, page, HK, D), 11).float() / ks).to(torch.float8_e4m3fn)
     vc8 = (_rand((nblocks, page, HK, D), 12).float() / vs).to(torch.float8_e4m3fn)
     q = _rand((B, 1, H, D), 13)
-    seqlens = torch.full((B,), S, dtype=torch.int32, device=DEV)
+    if ragged:
+        lens = torch.randint(1, S + 1, (B,), generator=torch.Generator().manual_seed(0))
+    else:
+        lens = torch.full((B,), S)
+    seqlens = lens.to(torch.int32).to(DEV)
     out, lse = xfa.flash_attn_with_kvcache(q, kc8, vc8, cache_seqlens=seqlens,
                                            block_table=table.to(DEV), k_scale=ks, v_scale=vs,
                                            return_softmax_lse=True)
@@ -162,13 +168,15 @@ def test_c5_full_shape(xfa, parity_report):
         # gather this sequence's pages (as bytes), dequantise exactly: f32(fp8) * 2^-4 -> bf16
         kd = (k8u[idx[b]].view(torch.float8_e4m3fn).float() * ks).bfloat16()
         vd = (v8u[idx[b]].view(torch.float8_e4m3fn).float() * vs).bfloat16()
-        kd, vd = kd.reshape(1, S, HK, D).cpu(), vd.reshape(1, S, HK, D).cpu()
+        n = int(lens[b])
+        kd, vd = kd.reshape(1, S, HK, D)[:, :n].cpu(), vd.reshape(1, S, HK, D)[:, :n].cpu()
         qs = q[b:b + 1].cpu()
         ref, _ = orc.attention_ref(qs, kd, vd)
         pt, _ = orc.attention_ref(qs, kd, vd, upcast=False, reorder_ops=True)
-        _check(parity_report, f"C5 out b{b}", out[b:b + 1], ref, pt, 3.0, 1e-5)
+        tag = f"C5{' ragged' if ragged else ''} b{b} len{n}"
+        _check(parity_report, f"{tag} out", out[b:b + 1], ref, pt, 3.0, 1e-5)
         lref = orc.attention_lse_ref(qs, kd)
         lerr = (lse[b:b + 1].cpu() - lref).abs().max().item()
-        parity_report({"case": f"C5 lse b{b}", "err": lerr, "bound": LSE_ATOL_DEC,
+        parity_report({"case": f"{tag} lse", "err": lerr, "bound": LSE_ATOL_DEC,
                        "ok": lerr < LSE_ATOL_DEC})
         assert lerr < LSE_ATOL_DEC

@@ -74,7 +74,7 @@ def test_dropout_keep_rate(xfa):
     (1, 4, 1, 160, 160, 128, False, (40, 10)),
     (2, 2, 2, 96, 256, 256, True, (-1, -1)),
 ])
-def test_dropout_fwd_bwd_vs_oracle(xfa, dtype, b, h, hk, sq, sk, d, causal, window):
+def test_dropout_fwd_bwd_vs_oracle(xfa, parity_report, dtype, b, h, hk, sq, sk, d, causal, window):
     torch.manual_seed(2)
     p = 0.2
     q = torch.randn(b, sq, h, d, dtype=dtype)
@@ -98,10 +98,13 @@ def test_dropout_fwd_bwd_vs_oracle(xfa, dtype, b, h, hk, sq, sk, d, causal, wind
     (o_ref, attn_ref, g_ref), (o_pt, attn_pt, g_pt) = refs
     err = (out.float().cpu() - o_ref.float()).abs().max().item()
     bound = 2 * (o_pt.float() - o_ref.float()).abs().max().item()
+    case = f"dropout p{p} b{b} h{h}/{hk} {sq}x{sk} d{d} causal={causal} window={window} {dtype}"
+    parity_report({"case": case + " out", "err": err, "bound": bound, "ok": err <= bound})
     assert err <= bound, (err, bound)
     for name, a, r, pt in zip(("dq", "dk", "dv"), (dq, dk, dv), g_ref, g_pt):
         e = (a.float().cpu() - r.float()).abs().max().item()
         bnd = 3 * (pt.float() - r.float()).abs().max().item() + 1e-5
+        parity_report({"case": f"{case} {name}", "err": e, "bound": bnd, "ok": e <= bnd})
         assert e <= bnd, (name, e, bnd)
     # the returned softmax (P normalised, sign = dropped) against the oracle's probabilities
     sm = s[:, :, :sq, :sk].float().abs().cpu()

@@ -18,7 +18,7 @@ Derivations (MI355X_MICROARCH.md):
     for 16-B/lane stores and float atomics; both in KiB;
   * SQ_WAIT_ANY / SQ_WAVE_CYCLES = fraction of wave time parked on s_waitcnt / barriers.
 
-  python tools/pmc_report.py gpurun_out/prof r02 fwd fwdbwd varlen decode
+  python tools/pmc_report.py gpurun_out/prof r03 fwd fwdbwd varlen decode fwd_fp8
 """
 import collections
 import csv
@@ -58,6 +58,16 @@ def stats(d):
     return (list(csv.DictReader(open(f[0]))), f[0]) if f else ([], None)
 
 
+def trace_median_ns(d, kernel):
+    """Median dispatch duration (ns) of `kernel` from the kernel-trace csv of the stats run."""
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not f:
+        return None
+    ds = sorted(float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                for r in csv.DictReader(open(f[0])) if r["Kernel_Name"] == kernel)
+    return ds[len(ds) // 2] if ds else None
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "")[:120]
 
@@ -70,6 +80,7 @@ def main():
         if sf:
             shutil.copy(sf, os.path.join("profiles", f"{tag}_{m}_kernel_stats.csv"))
         dom = max(rows, key=lambda r: float(r["TotalDurationNs"])) if rows else None
+        med = trace_median_ns(os.path.join(root, f"{m}_stats"), dom["Name"]) if dom else None
         merged = collections.defaultdict(dict)
         for p in ("sq1", "sq2", "fetch", "write"):
             for k, cs in counters(os.path.join(root, f"{m}_{p}")).items():
@@ -109,12 +120,13 @@ def main():
             res[short(k)] = e
         pmc[m] = {"dominant_kernel": short(dom["Name"]) if dom else None,
                   "dominant_avg_ns": float(dom["AverageNs"]) if dom else None,
+                  "dominant_median_ns": med,
                   "dominant_calls": int(dom["Calls"]) if dom else None,
                   "kernels": res}
         if dom:
             key = next((k for k in res if k == short(dom["Name"])), None)
             if key and "hbm_bytes_per_launch" in res[key]:
-                traffic[m] = {"kernel": key, "avg_ns": float(dom["AverageNs"]),
+                traffic[m] = {"kernel": key, "avg_ns": float(dom["AverageNs"]), "median_ns": med,
                               "calls": int(dom["Calls"]),
                               "hbm_bytes_per_launch": res[key]["hbm_bytes_per_launch"],
                               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + "
