@@ -5,6 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("--opt", action="append", default=[])
 ap.add_argument("--bf16", action="store_true")
+ap.add_argument("--ragged", action="store_true", help="cache lengths U[1, S] (bench.py --ragged)")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
@@ -17,16 +18,18 @@ nb = B * S // page
 table = torch.randperm(nb, device="cuda").to(torch.int32).view(B, S // page)
 q = torch.randn(B, 1, H, D, device="cuda", dtype=torch.bfloat16)
 lens = torch.full((B,), S, dtype=torch.int32, device="cuda")
+if a.ragged:
+    lens = torch.randint(1, S + 1, (B,), generator=torch.Generator().manual_seed(0)).to(torch.int32).cuda()
 if a.bf16:
     kc = torch.randn(nb, page, HK, D, device="cuda", dtype=torch.bfloat16)
     vc = torch.randn(nb, page, HK, D, device="cuda", dtype=torch.bfloat16)
     run = lambda: xfa.flash_attn_with_kvcache(q, kc, vc, cache_seqlens=lens, block_table=table)
-    nbytes = 2 * B * S * HK * D * 2
+    nbytes = 2 * int(lens.sum()) * HK * D * 2
 else:
     kc = (torch.randn(nb, page, HK, D, device="cuda") * 4).to(torch.float8_e4m3fn).view(torch.uint8)
     vc = (torch.randn(nb, page, HK, D, device="cuda") * 4).to(torch.float8_e4m3fn).view(torch.uint8)
     run = lambda: pa.fwd_kvcache_fp8(q, kc, vc, lens, table, 0.25, 0.25, D ** -0.5, False, -1, -1, 0)
-    nbytes = 2 * B * S * HK * D
+    nbytes = 2 * int(lens.sum()) * HK * D
 variants = [[]]
 for spec in a.opt:
     n, vals = spec.split("=")

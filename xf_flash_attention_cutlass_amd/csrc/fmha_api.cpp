@@ -282,14 +282,26 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     if (!p.decode) splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
     p.num_splits = splits;
     g_last_splits = splits;
+    // Ragged caches (per-sequence lengths): the b * splits slots of a kv-head group are shared
+    // in proportion to the sequences' key tiles, up to 128 splits for one sequence
+    // (fmha_decode_kernel.h dec_slot); equal lengths give the same splits as without.
+    p.dec_bal = p.decode && o.dec_bal.load() && !o.dec_fold.load() && p.dec_hmaj >= 1 &&
+                p.seqused_k && p.b >= 2 && p.b <= 64;
+    p.dec_slots = p.dec_bal ? p.b * splits : 0;
+    p.dec_cap = p.dec_bal ? std::min(p.dec_slots, 128) : 0;
+    p.dec_ns = nullptr;
+    const int ext = p.dec_bal ? p.dec_cap : splits;   // split extent of the scratch
     if (splits > 1) {
         const int hd = hd_bucket(p.d);
         const size_t rows = (size_t)p.b * p.h * p.seqlen_q;
-        const size_t bytes = (size_t)splits * rows * (hd + 1) * sizeof(float);
+        const size_t obytes = (size_t)ext * rows * hd * sizeof(float);
+        const size_t lbytes = (size_t)ext * rows * sizeof(float);
+        const size_t bytes = obytes + lbytes + (p.dec_bal ? (size_t)p.b * sizeof(int) : 0);
         char* base = (char*)pool_get(st, bytes);
         if (!base) { fail(3, "could not allocate %zu bytes of split scratch", bytes); return; }
         p.oaccum = (float*)base;
-        p.lseaccum = (float*)(base + (size_t)splits * rows * hd * sizeof(float));
+        p.lseaccum = (float*)(base + obytes);
+        if (p.dec_bal) p.dec_ns = (int*)(base + obytes + lbytes);
     }
     p.dec_ctr = nullptr;
     if (p.decode && o.dec_fold.load()) {
@@ -331,7 +343,7 @@ int fmha_set_option(const char* name, int value) {
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 3},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
-        {"dec_fold", &o.dec_fold, 0, 1},
+        {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -355,7 +367,7 @@ int fmha_get_option(const char* name) {
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
     XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
-    XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold)
+    XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold) XFA_GET(dec_bal)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;

@@ -121,6 +121,10 @@ struct FwdParams {
     int* work_ctr;             // persistent == 3: self-resetting counters [-, finished, next x 8]
     int* dec_ctr;              // decode, combine folded in: per (batch, kv head) split arrival
                                // counters (zero between launches: the merging wave resets its own)
+    int dec_bal;               // decode over ragged caches: split slots shared in proportion to
+                               // the sequences' key tiles (fmha_decode_kernel.h dec_slot)
+    int dec_slots, dec_cap;    // dec_bal: slots per kv-head group; max splits of one sequence
+    int* dec_ns;               // dec_bal: [b] split count of each sequence (for the combine)
     int xcd_queues;            // persistent == 3: one item queue per XCD (else queue 0 only)
     // host-side launch choices (snapshotted from the options by the C ABI, per call)
     int waves;                 // 4 or 8 waves per workgroup (D <= 128)
@@ -147,6 +151,7 @@ struct CombineParams {
     int64_t o_batch, o_row, o_head;
     int64_t lse_batch, lse_head;
     int b, h, seqlen_q, d, hd, num_splits;
+    const int* dec_ns;   // per-batch split counts (balanced decode), or null: num_splits
 };
 
 struct BwdParams {

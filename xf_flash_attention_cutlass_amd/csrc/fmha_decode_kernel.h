@@ -77,6 +77,63 @@ __device__ __forceinline__ float quad_sum16(float x) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Key tiles of sequence `b` that some query row can see (the union of the rows' windows):
+// [t_first, t_end) in kDecKeys-key tiles; the decode kernel cuts exactly this range into splits.
+__device__ __forceinline__ int2 dec_tile_range(const FwdParams& p, const int b) {
+    const int lp = p.leftpad_k ? p.leftpad_k[b] : 0;
+    const int sk = (p.seqused_k ? p.seqused_k[b] : p.seqlen_k) - lp;
+    const int rows = p.seqlen_q * p.group;
+    const int diag = sk - p.seqlen_q;
+    const int last = rows > 0 ? (rows - 1) / p.group : 0;
+    const int k_lo = p.wl >= 0 ? max(0, diag - p.wl) : 0;
+    const int k_hi = p.wr >= 0 ? min(sk, last + diag + p.wr + 1) : sk;
+    const int t_first = k_lo / kDecKeys;
+    const int t_end = k_hi > k_lo ? (k_hi + kDecKeys - 1) / kDecKeys : t_first;
+    return int2{t_first, t_end};
+}
+
+// Balanced split allocation over ragged caches (`dec_bal`): the p.dec_slots split slots of one
+// kv-head group are shared by the sequences in proportion to their key tiles, at least one each
+// and at most p.dec_cap (the scratch's split extent): sequence b owns slots
+// [S_b, S_b + n_b) with n_b = 1 + floor(E (C_b + T_b) / T) - floor(E C_b / T), E = slots - B,
+// C_b = the tiles of the sequences before b, T = all tiles.  Equal lengths give n_b =
+// slots / B, i.e. the per-sequence split of the uniform launch (same ranges, same result).
+// Lane b computes sequence b's share (b < B <= 64, one vector load of the lengths), the
+// prefix sums run across the wave.  Slot f -> (sequence, split, n_b); false for a slot past the
+// last sequence's.
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned x, const int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ bool dec_slot(const FwdParams& p, const int f, const int lane,
+                                         int& bidx, int& split, int& nsb) {
+    const bool own = lane < p.b;
+    unsigned tb = 0;
+    if (own) {
+        const int2 r = dec_tile_range(p, lane);
+        tb = (unsigned)(r.y - r.x);
+    }
+    const unsigned incl = wave_incl_scan(tb, lane);
+    const uint64_t total = __shfl(incl, 63);
+    const uint64_t extra = (uint64_t)(p.dec_slots - p.b);
+    int n = 0;
+    if (own) {
+        n = 1 + (total > 0 ? (int)(extra * incl / total - extra * (incl - tb) / total) : 0);
+        n = min(n, p.dec_cap);
+    }
+    const unsigned send = wave_incl_scan((unsigned)n, lane);
+    const uint64_t hit = __ballot(own && (unsigned)f < send);
+    if (!hit) return false;
+    bidx = __builtin_ctzll(hit);
+    nsb = __shfl(n, bidx);
+    split = f - (int)(__shfl(send, bidx) - (unsigned)nsb);
+    return true;
+}
+
 template <int HD, typename T, bool KV8, int MR, int NWV = kDecWaves>
 __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParams p) {
     using V8 = typename DT<T>::v8;
@@ -102,8 +159,19 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
     const int hh = lane / MR;                     // key sub-block (0..64/MR-1) of this lane
     // wave -> (batch, kv head, split): 4 splits of one kv head, or (dec_hmaj) 4 kv heads of one
     // split, whose rows sit side by side in each cache row (HD * ESZ bytes apart)
-    int bidx, hk_i, split;
-    if (p.dec_hmaj) {
+    int bidx, hk_i, split, nsplit = p.num_splits;
+    if (p.dec_bal) {
+        // the head-major grid; slot f = x-batch * num_splits + y (for equal lengths exactly the
+        // head-major launch's (batch, split), dispatched in the same order) -> (sequence, split)
+        const int g4 = p.hk / NWV;
+        const int xb = blockIdx.x / g4;
+        hk_i = (blockIdx.x - xb * g4) * NWV + wave;
+        if (!dec_slot(p, xb * p.num_splits + blockIdx.y, lane, bidx, split, nsplit)) return;
+        bidx = __builtin_amdgcn_readfirstlane(bidx);
+        split = __builtin_amdgcn_readfirstlane(split);
+        nsplit = __builtin_amdgcn_readfirstlane(nsplit);
+        if (split == 0 && hk_i == 0 && lane == 0) p.dec_ns[bidx] = nsplit;  // for the combine
+    } else if (p.dec_hmaj) {
         const int g4 = p.hk / NWV;
         bidx = blockIdx.x / g4;
         hk_i = (blockIdx.x - bidx * g4) * NWV + wave;
@@ -139,7 +207,7 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
     const int k_lo = lim_l(0), k_hi = lim_r(rows > 0 ? (rows - 1) / G : 0);
     const int t_first = k_lo / kDecKeys;
     const int t_end = k_hi > k_lo ? (k_hi + kDecKeys - 1) / kDecKeys : t_first;
-    const int per = (t_end - t_first + p.num_splits - 1) / p.num_splits;
+    const int per = (t_end - t_first + nsplit - 1) / nsplit;
     const int t_lo = min(t_end, t_first + split * per);
     const int t_hi = min(t_end, t_lo + per);
 

@@ -37,6 +37,7 @@ static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
     cp.lse_batch = p.lse_batch; cp.lse_head = p.lse_head;
     cp.b = p.b; cp.h = p.h; cp.seqlen_q = p.seqlen_q; cp.d = p.d; cp.hd = hd;
     cp.num_splits = p.num_splits;
+    cp.dec_ns = p.decode && p.dec_bal ? p.dec_ns : nullptr;
     const int64_t crow = (int64_t)p.b * p.h * p.seqlen_q;
     hipLaunchKernelGGL(kern, dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
     return hipGetLastError();

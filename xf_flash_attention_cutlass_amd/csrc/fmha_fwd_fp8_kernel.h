@@ -292,6 +292,46 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
         __builtin_amdgcn_sched_barrier(0);
     };
     const int lim_e = my_lr - 4 * hh;
+    // Pipeline softmax without a row max per tile (the 4-wave bf16 kernel's scheme,
+    // fmha_fwd4_kernel.h): P = exp2(X) against the running max m_sc; a tile whose per-lane
+    // partial row sum passes 2^slack (slack <= 8: every P <= 256 < 448, the e4m3 maximum)
+    // re-runs its softmax against its true row max after rescaling O and l (rare).  The
+    // shifts X = S c - m and the row sums run on packed fp32 (v_pk_fma_f32 / v_pk_add_f32).
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    const float thr = __builtin_amdgcn_exp2f(fminf(p.max_slack, 8.f));
+    auto exp_dword = [&](const f32x16 (&x)[2], const int kt, const int d, f2& ra, f2& rb) {
+        const float e0 = fast_exp2(x[kt][4 * d]), e1 = fast_exp2(x[kt][4 * d + 1]);
+        const float e2 = fast_exp2(x[kt][4 * d + 2]), e3 = fast_exp2(x[kt][4 * d + 3]);
+        ra += f2{e0, e1};
+        rb += f2{e2, e3};
+        const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
+        return __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
+    };
+    // the rare path: X -= its true row max (or the running max catches up), O and l rescaled,
+    // P and the row sums of this tile recomputed
+    auto redo = [&](f32x16 (&x)[2], int (&pw)[2][4], f2& ra, f2& rb) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < 32; ++v) mx = fmaxf(mx, x[v >> 4][v & 15]);
+        mx = wave_max_halves(mx);
+        const bool fresh = m_sc == -INFINITY;
+        const float delta = fresh ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
+        const float alpha = fresh ? 1.f : fast_exp2(-delta);
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
+#pragma unroll
+        for (int v = 0; v < 32; ++v) x[v >> 4][v & 15] -= delta;
+        m_sc = fresh ? (mx == -INFINITY ? -INFINITY : mx) : m_sc + delta;
+        ra = f2{0.f, 0.f};
+        rb = f2{0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) pw[kt][d] = exp_dword(x, kt, d, ra, rb);
+    };
     auto pipe_range = [&](const int lo, const int hm, const int hi) {
         const bool third = lo + 2 < hi;
         dma_tile(lo, 0);
@@ -343,7 +383,7 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
             sn[0] = f32x16{};
             sn[1] = f32x16{};
             int pw[2][4];
-            float rs0 = 0.f, rs1 = 0.f;
+            f2 ra = {0.f, 0.f}, rb = {0.f, 0.f};
             i32x8 ka = rd_k(ks, 0, 0);
             static_for<4>([&](auto M) {
                 constexpr int m = decltype(M)::value;    // MFMA m: key half m >> 1, d half m & 1
@@ -352,21 +392,21 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
                 sn[m >> 1] = mfma_fp8(ka, qf[m & 1], sn[m >> 1]);
                 // exp values of dwords (kt = m >> 1, d = 2 (m & 1), 2 (m & 1) + 1)
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int kt = m >> 1, d = 2 * (m & 1) + u;
-                    const float e0 = fast_exp2(st[kt][4 * d]), e1 = fast_exp2(st[kt][4 * d + 1]);
-                    const float e2 = fast_exp2(st[kt][4 * d + 2]), e3 = fast_exp2(st[kt][4 * d + 3]);
-                    rs0 += e0 + e1;
-                    rs1 += e2 + e3;
-                    const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
-                    pw[kt][d] = __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
-                }
+                for (int u = 0; u < 2; ++u)
+                    pw[m >> 1][2 * (m & 1) + u] = exp_dword(st, m >> 1, 2 * (m & 1) + u, ra, rb);
                 // keep the row-sum adds in this MFMA gap (fmha_fwd_kernel.h: else sunk below
                 // phase b)
-                asm volatile("" : "+v"(rs0), "+v"(rs1));
+                asm volatile("" : "+v"(ra), "+v"(rb));
                 ka = kn;
                 __builtin_amdgcn_sched_barrier(0);
             });
+            {
+                const f2 rab = ra + rb;
+                if (__any(rab[0] + rab[1] > thr || m_sc == -INFINITY)) {
+                    asm volatile("; redo_p");
+                    redo(st, pw, ra, rb);
+                }
+            }
             i32x8 pb;
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
@@ -377,7 +417,7 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
             // phase b: O += V_j^T P_j (4 MFMAs, V^T read one MFMA ahead) beside
             // X_{j+1} = S_{j+1} c - m and its row max (8 values per MFMA)
             const float mr = m_sc == -INFINITY ? 0.f : m_sc;
-            float mx = -INFINITY;
+            const f2 c2 = {c, c}, m2 = {-mr, -mr};
             i32x8 va = rd_v_asm(std::integral_constant<int, vs * TILE>{}, 0);
             static_for<ND>([&](auto D) {
                 constexpr int dt = decltype(D)::value;
@@ -390,42 +430,26 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
                 }
                 acc_o[dt] = mfma_fp8(va, pb, acc_o[dt]);
 #pragma unroll
-                for (int v = 8 * dt; v < 8 * dt + 8; ++v)
-                    sn[v >> 4][v & 15] = __builtin_fmaf(sn[v >> 4][v & 15], c, -mr);
-#pragma unroll
-                for (int v = 8 * dt; v < 8 * dt + 8; v += 2)
-                    mx = fmaxf(fmaxf(mx, sn[v >> 4][v & 15]), sn[(v + 1) >> 4][(v + 1) & 15]);
+                for (int v = 8 * dt; v < 8 * dt + 8; v += 2) {
+                    f2 x = {sn[v >> 4][v & 15], sn[v >> 4][(v & 15) + 1]};
+                    x = __builtin_elementwise_fma(x, c2, m2);
+                    sn[v >> 4][v & 15] = x[0];
+                    sn[v >> 4][(v & 15) + 1] = x[1];
+                }
                 va = vn;
                 __builtin_amdgcn_sched_barrier(0);
             });
-            asm volatile("" : "+v"(mx));
-            l_run += rs0 + rs1;
-            if (j + 1 >= hm) {               // edge tile: mask, then the row max again
+            {
+                const f2 rab = ra + rb;
+                l_run += rab[0] + rab[1];
+            }
+            if (j + 1 >= hm) {               // edge tile: mask in registers
                 const int lim_t = lim_e - (j + 1) * kBlockN;
-                float mm = -INFINITY;
 #pragma unroll
                 for (int v = 0; v < 32; ++v) {
                     const int off = 32 * (v >> 4) + ((v & 15) & 3) + 8 * ((v & 15) >> 2);
                     if (off >= lim_t) sn[v >> 4][v & 15] = -INFINITY;
-                    mm = fmaxf(mm, sn[v >> 4][v & 15]);
                 }
-                mx = mm;
-            }
-            // deferred rescale on the shifted scores (fmha_fwd_kernel.h rescale_x)
-            mx = wave_max_halves(mx);
-            const bool fresh = m_sc == -INFINITY;
-            if (__any(mx > p.max_slack || (fresh && mx != -INFINITY))) {
-                asm volatile("; rescale_x");
-                const float delta = fresh ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
-                const float alpha = fresh ? 1.f : fast_exp2(-delta);
-                l_run *= alpha;
-#pragma unroll
-                for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc_o[dt][r] *= alpha;
-#pragma unroll
-                for (int v = 0; v < 32; ++v) sn[v >> 4][v & 15] -= delta;
-                m_sc = fresh ? (mx == -INFINITY ? -INFINITY : mx) : m_sc + delta;
             }
             publish(issue);
         };
@@ -450,21 +474,22 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
             ++r;
         }
         // drain: the wave's last tile's softmax and PV (its X is in sb after an odd step count)
-        f32x16 (&sl)[2] = (nsteps_w & 1) ? sb : sa;
+        // (a register copy: redo() writes it, and a runtime-selected array reference would
+        // live in scratch)
+        const bool odd = nsteps_w & 1;
+        f32x16 sl[2] = {odd ? sb[0] : sa[0], odd ? sb[1] : sa[1]};
         int pw[2][4];
-        float rs0 = 0.f, rs1 = 0.f;
+        f2 ra = {0.f, 0.f}, rb = {0.f, 0.f};
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const float e0 = fast_exp2(sl[kt][4 * d]), e1 = fast_exp2(sl[kt][4 * d + 1]);
-                const float e2 = fast_exp2(sl[kt][4 * d + 2]), e3 = fast_exp2(sl[kt][4 * d + 3]);
-                rs0 += e0 + e1;
-                rs1 += e2 + e3;
-                const int w = __builtin_amdgcn_cvt_pk_fp8_f32(e0, e1, 0, false);
-                pw[kt][d] = __builtin_amdgcn_cvt_pk_fp8_f32(e2, e3, w, true);
-            }
-        l_run += rs0 + rs1;
+            for (int d = 0; d < 4; ++d) pw[kt][d] = exp_dword(sl, kt, d, ra, rb);
+        {
+            const f2 rab = ra + rb;
+            if (__any(rab[0] + rab[1] > thr || m_sc == -INFINITY)) redo(sl, pw, ra, rb);
+            const f2 rab2 = ra + rb;
+            l_run += rab2[0] + rab2[1];
+        }
         i32x8 pb;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {

@@ -824,7 +824,7 @@ __global__ void __launch_bounds__(256) fmha_combine_kernel(const CombineParams c
     const int pos = (int)(rid % cp.seqlen_q);
     const int head = (int)((rid / cp.seqlen_q) % cp.h);
     const int bidx = (int)(rid / ((int64_t)cp.seqlen_q * cp.h));
-    const int ns = cp.num_splits;
+    const int ns = cp.dec_ns ? cp.dec_ns[bidx] : cp.num_splits;
     float mx = -INFINITY;
     for (int s = lane; s < ns; s += 64) mx = fmaxf(mx, cp.lseaccum[s * rows + rid]);
     mx = wave_max_halves(mx);

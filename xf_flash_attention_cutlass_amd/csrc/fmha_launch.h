@@ -29,6 +29,8 @@ struct Options {
     std::atomic<int> dec_mr{16};         // decode MFMA rows: 16 when the query rows fit 16 (C5: 105 vs
                                          // 110 us with dec_hmaj = 1), else 32
     std::atomic<int> dec_fold{0};        // decode: the last split of each (b, kv head) merges the partials
+    std::atomic<int> dec_bal{1};         // decode over per-sequence cache lengths (2 <= b <= 64): split
+                                         // slots shared in proportion to the key tiles (ragged caches)
                                          // (no separate combine launch; C5: 126.8 vs 105.5 us - the
                                          // coherent partial stores and the 64-wave merge tail cost
                                          // more than the 5 us combine launch they replace)
