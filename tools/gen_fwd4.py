@@ -57,14 +57,35 @@ VREG = 4 * TILE       # V ring after the K ring
 QK_LEAD = 6           # QK MFMAs before the first PV MFMA (the step's V^T reads land meanwhile)
 READ_LEAD = 5         # gaps between an LDS read and the MFMA that consumes it
 
-# fixed registers
+# fixed registers (PS: the pre-scaled body, see set_mode; the map below is the legacy one)
 SBASE = (0, 64)       # S buffers A, B
 PBASE = (128, 160)    # P buffers A, B
 TMP = 192             # 8 scratch
 LT, LIM, NM, LRUN = 200, 202, 204, 206
 MISC = 208            # 208..215: 213 = +inf, 214 = -inf
 PINF, NINF = 213, 214
+NMB = None            # PS: v[NMB + 16 rb : +15] = -m of row block rb (the S MFMA chains' C operand)
+NVFIX = 216           # fixed VGPRs v[0:NVFIX-1]
+PS = False
 ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 192, 240
+
+
+def set_mode(ps):
+    """PS (default): Q is scaled by c = softmax_scale * log2(e) once per item (bf16 / fp16
+    rounding of c q, finer than the reference's own q / sqrt(d) rounding in its low-precision
+    oracle) and every QK^T chain starts from C = -m instead of 0, so the MFMA hands the softmax
+    s c - m directly: one v_exp per score, no fma.  Legacy: P = exp2(fma(s, c, -m))."""
+    global PS, TMP, LT, LIM, NM, LRUN, MISC, PINF, NINF, NMB, NVFIX
+    PS = ps
+    if ps:
+        NMB = 192                         # v[192:223]
+        TMP = 224                         # 4 scratch (exp results; the raw S stays for the rare path)
+        LT, LIM, NM, LRUN = 228, 230, 232, 234
+        MISC = PINF = NINF = None         # temps from dead buffers, -inf as a literal
+        NVFIX = 236
+    else:
+        NMB = None
+        TMP, LT, LIM, NM, LRUN, MISC, PINF, NINF, NVFIX = 192, 200, 202, 204, 206, 208, 213, 214, 216
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94     # SRA: s[92:93], SCM: s[94:95]
 SKR, SVR = 80, 84     # s[80:83] / s[84:87]: the K / V buffer descriptors of this step's DMA tiles
 
@@ -138,23 +159,31 @@ def sm_value_ops(dt, v, src_buf, dst_buf, mask, nt):
     """the softmax ops of score v: [(stage, [texts])], stage 0 fma, 1 exp(+mask), 2 add, 3 cvt"""
     rb, kt, r, off, dword = value_info(v)
     t = f"v{TMP + v % nt}"
-    ops = [(0, [f"v_fma_f32 {t}, {se(src_buf, v)}, %[c], v{NM + rb}"])]
-    ex = [f"v_exp_f32 {t}, {t}"]
+    if PS:
+        # the score already is s c - m: exp into a scratch (the raw S stays for the rare path)
+        z = 0
+        ex = [f"v_exp_f32 {t}, {se(src_buf, v)}"]
+        ops = []
+    else:
+        z = 1
+        ops = [(0, [f"v_fma_f32 {t}, {se(src_buf, v)}, %[c], v{NM + rb}"])]
+        ex = [f"v_exp_f32 {t}, {t}"]
     if mask:
         ex += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}", f"v_cndmask_b32 {t}, 0, {t}, vcc"]
-    ops.append((1, ex))
+    ops.append((z, ex))
     if v % 32 == 0:
-        ops.append((2, [f"v_mov_b32 v{LT + rb}, {t}"]))
+        ops.append((z + 1, [f"v_mov_b32 v{LT + rb}, {t}"]))
     else:
-        ops.append((2, [f"v_add_f32 v{LT + rb}, v{LT + rb}, {t}"]))
+        ops.append((z + 1, [f"v_add_f32 v{LT + rb}, v{LT + rb}, {t}"]))
     if v & 1:
         tp = f"v{TMP + (v - 1) % nt}"
-        ops.append((2, [f"v_cvt_pk_{dt}_f32 {pe(dst_buf, dword)}, {tp}, {t}"]))
+        ops.append((z + 1, [f"v_cvt_pk_{dt}_f32 {pe(dst_buf, dword)}, {tp}, {t}"]))
     return ops
 
 
-def step_body(dt, ph, kind, mask):
-    """instructions of one step at ring phase ph (= j mod 4)"""
+def step_body(dt, ph, kind, mask, use_nm=True):
+    """instructions of one step at ring phase ph (= j mod 4); use_nm: (PS) the QK^T chains
+    start from C = -m (False only for tile 0, whose m is not known yet)"""
     par = ph & 1
     sn_buf, sc_buf = (0, 1) if par == 0 else (1, 0)      # S_{j+2} -> sn, scores of j+1 in sc
     pc_buf, pn_buf = (0, 1) if par == 0 else (1, 0)      # P_j in pc, P_{j+1} -> pn
@@ -176,7 +205,7 @@ def step_body(dt, ph, kind, mask):
             s, kt = a, b
             f = 2 * s + kt
             acc = sv(sn_buf, rb * 2 + kt)
-            src = "0" if s == 0 else acc
+            src = acc if s else (f"v[{NMB + 16 * rb}:{NMB + 16 * rb + 15}]" if PS and use_nm else "0")
             mfma[g] = f"{mnem} {acc}, {ktup(f % 4)}, {qtup(rb, s)}, {src}"
             kfirst.setdefault(f, g); klast[f] = g
             need[g] = ("K", f)
@@ -216,7 +245,7 @@ def step_body(dt, ph, kind, mask):
                 f"buffer_load_dwordx4 %[dma{i}], {srd}, 0 offen lds"]
 
     dmas = [(w, i) for i in range(4) for w in ("K", "V")]
-    nt = 4 if G in (0, 64) else 8
+    nt = 4 if (G in (0, 64) or PS) else 8
     sm = []      # (gap, seq, texts)
     if kind & SM:
         span = G if G else 64
@@ -275,6 +304,8 @@ def step_body(dt, ph, kind, mask):
         else:
             # past the last MFMA nothing separates a gap's v_exp from the next gap's use of its
             # result: a VALU reading a transcendental's result needs one wait state
+            if not (smby.get(g) or dma_gap.get(g) or rby.get(g)):
+                continue
             body.append("s_nop 0")
         dm = dma_gap.get(g, [])
         body += [dma(w, i)[0] for w, i in dm]
@@ -347,6 +378,58 @@ def redo_block(dt, par, uid):
     return out
 
 
+def redo_block_ps(dt, par, uid):
+    """PS rare path for the scores in buffer sc (s c - m_old): d = max(0, masked tile max);
+    m += d (NM, the C blocks), O and l scaled by 2^-d, the tile's scores and the next tile's
+    (already in sn, computed against m_old) shifted by -d, the tile's softmax redone.  Temps
+    come from the P buffer of tile j (consumed by this step's PV)."""
+    sc_buf = 1 if par == 0 else 0
+    sn_buf = 1 - sc_buf
+    pn_buf = 1 if par == 0 else 0
+    pc = PBASE[1 - pn_buf]
+    out = [f".Lredo{par}_{uid}:", "s_nop 7", "s_nop 7", "s_nop 3"]
+    mx, t2, dl, alpha, ninf = (f"v{pc + 8 + i}" for i in range(5))
+    out.append(f"v_mov_b32 {ninf}, 0xff800000")
+    for rb in (0, 1):
+        out.append(f"v_mov_b32 {mx}, {ninf}")
+        for vv in range(32):
+            v = rb * 32 + vv
+            _, _, _, off, _ = value_info(v)
+            out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}",
+                    f"v_cndmask_b32 {t2}, {ninf}, {se(sc_buf, v)}, vcc",
+                    f"v_max_f32 {mx}, {mx}, {t2}"]
+        out += [f"v_mov_b32 {t2}, {mx}", "s_nop 1", f"v_permlane32_swap_b32 {mx}, {t2}",
+                "s_nop 1",
+                f"v_max_f32 {mx}, {mx}, {t2}",
+                f"v_max_f32 {dl}, 0, {mx}",                  # d >= 0
+                f"v_exp_f32_e64 {alpha}, -{dl}",
+                f"v_sub_f32 v{NM + rb}, v{NM + rb}, {dl}",
+                "s_nop 0",
+                f"v_mul_f32 v{LRUN + rb}, v{LRUN + rb}, {alpha}"]
+        out += [f"v_mov_b32 v{NMB + 16 * rb + i}, v{NM + rb}" for i in range(16)]
+        for vv in range(32):
+            v = rb * 32 + vv
+            out += [f"v_sub_f32 {se(sc_buf, v)}, {se(sc_buf, v)}, {dl}",
+                    f"v_sub_f32 {se(sn_buf, v)}, {se(sn_buf, v)}, {dl}"]
+        for i in range(64):
+            a = f"a{ABASE_O + 64 * rb + i}"
+            t = f"v{pc + i % 8}"
+            out += [f"v_accvgpr_read_b32 {t}, {a}", f"v_mul_f32 {t}, {t}, {alpha}",
+                    f"v_accvgpr_write_b32 {a}, {t}"]
+        out.append("s_nop 1")
+        # the tile's softmax again, masked, against the new reference
+        ops = []
+        for vv in range(32):
+            v = rb * 32 + vv
+            for stage, txt in sm_value_ops(dt, v, sc_buf, pn_buf, True, 4):
+                ops.append((vv + stage, 4 * vv + stage, txt))
+        for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1])):
+            out += txt
+        out.append("s_nop 0")
+    out += ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    return out
+
+
 def redo_check(par, uid, tag):
     """after a step with SM: any lane's tile sum past the threshold -> rare path; l += tile sums"""
     return [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
@@ -402,8 +485,16 @@ def item_program(dt, uid="%="):
                 f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
     out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(dt, 3, QK | SM, False)
     out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
+    out += main_loop(dt, uid)
+    # rare path bodies
+    out += redo_block(dt, 0, uid) + redo_block(dt, 1, uid)
+    out += epilogue(dt, uid)
+    return out
+
+
+def main_loop(dt, uid):
     # main loop over steps j = 0 .. ntl-1, unrolled over the 4 ring phases
-    out += [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
+    out = [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
     for ph in range(4):
         par = ph & 1
         out.append(f".Lph{ph}_{uid}:")
@@ -424,12 +515,25 @@ def item_program(dt, uid="%="):
         out += [f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
                 f"s_cbranch_scc1 .Lexit_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
-    # rare path bodies
-    out += redo_block(dt, 0, uid) + redo_block(dt, 1, uid)
+    return out
+
+
+def epilogue(dt, uid):
     # epilogue: normalise, O rows (16-byte stores after a permlane32 exchange), LSE
-    out.append(f".Lexit_{uid}:")
+    out = [f".Lexit_{uid}:"]
     out += ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_nop 7", "s_nop 7", "s_nop 3"]
-    inv, L, t, lse = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}", f"v{MISC + 3}"
+    if PS:
+        # temps and the offsets (from their AGPR operands) in S buffer A above the store sets
+        inv, L, t, lse, cls, pinf = (f"v{56 + i}" for i in range(6))
+        oo, lo = ("v52", "v53"), ("v54", "v55")
+        out += [f"v_mov_b32 {pinf}, 0x7f800000",
+                f"v_accvgpr_read_b32 {oo[0]}, %[ooff0]", f"v_accvgpr_read_b32 {oo[1]}, %[ooff1]",
+                f"v_accvgpr_read_b32 {lo[0]}, %[loff0]", f"v_accvgpr_read_b32 {lo[1]}, %[loff1]",
+                "s_nop 1"]
+    else:
+        inv, L, t, lse = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}", f"v{MISC + 3}"
+        cls, pinf = f"v{MISC + 7}", f"v{PINF}"
+        oo, lo = ("%[ooff0]", "%[ooff1]"), ("%[loff0]", "%[loff1]")
     n = 0
     for rb in (0, 1):
         out += [f"v_mov_b32 {t}, v{LRUN + rb}", "s_nop 1", f"v_permlane32_swap_b32 v{LRUN + rb}, {t}",
@@ -437,13 +541,13 @@ def item_program(dt, uid="%="):
                 f"v_add_f32 {L}, v{LRUN + rb}, {t}",
                 f"v_rcp_f32 {inv}, {L}",
                 f"v_log_f32 {lse}, {L}",
-                f"v_mov_b32 v{MISC + 7}, 0x63",
-                f"v_cmp_class_f32 vcc, {L}, v{MISC + 7}",
+                f"v_mov_b32 {cls}, 0x63",
+                f"v_cmp_class_f32 vcc, {L}, {cls}",
                 f"v_cndmask_b32_e64 {inv}, {inv}, 1.0, vcc",
                 f"v_sub_f32 {lse}, {lse}, v{NM + rb}",
                 f"v_mul_f32 {lse}, 0x3f317218, {lse}",
-                f"v_cndmask_b32 {lse}, {lse}, v{PINF}, vcc",
-                f"buffer_store_dword {lse}, %[loff{rb}], %[lsrd], 0 offen"]
+                f"v_cndmask_b32 {lse}, {lse}, {pinf}, vcc",
+                f"buffer_store_dword {lse}, {lo[rb]}, %[lsrd], 0 offen"]
         for d in range(4):
             for gp in (0, 2):
                 vb = 0 if n % 2 == 0 else 32          # two alternating register sets (S buffer A)
@@ -461,13 +565,87 @@ def item_program(dt, uid="%="):
                         f"v_permlane32_swap_b32 v{w0}, v{w0 + 2}",
                         f"v_permlane32_swap_b32 v{w0 + 1}, v{w0 + 3}",
                         "s_nop 1",
-                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], %[ooff{rb}], %[osrd], 0 offen offset:{64 * d + 16 * gp}",
+                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], {oo[rb]}, %[osrd], 0 offen offset:{64 * d + 16 * gp}",
                         "s_nop 1"]
     return out
 
 
+def q_prescale(dt):
+    """PS: Q <- dt(c q) in place (fp32 product, one rounding), 16 dwords per batch through the
+    S buffers (free until the first QK^T)"""
+    out = []
+    for b0 in range(0, 64, 16):
+        regs = range(b0, b0 + 16)
+        out += [f"v_accvgpr_read_b32 v{i}, a{ABASE_Q + i}" for i in regs]
+        for i in regs:
+            lo, hi = f"v{64 + i}", f"v{128 + i}"
+            if dt == "bf16":
+                out += [f"v_lshlrev_b32 {lo}, 16, v{i}", f"v_and_b32 {hi}, 0xffff0000, v{i}"]
+            else:
+                out += [f"v_cvt_f32_f16 {lo}, v{i}", f"v_lshrrev_b32 {hi}, 16, v{i}",
+                        f"v_cvt_f32_f16 {hi}, {hi}"]
+        out += [f"v_mul_f32 v{64 + i}, %[c], v{64 + i}" for i in regs]
+        out += [f"v_mul_f32 v{128 + i}, %[c], v{128 + i}" for i in regs]
+        out += [f"v_cvt_pk_{dt}_f32 v{i}, v{64 + i}, v{128 + i}" for i in regs]
+        out += [f"v_accvgpr_write_b32 a{ABASE_Q + i}, v{i}" for i in regs]
+    out.append("s_nop 1")
+    return out
+
+
+def item_program_ps(dt, uid="%="):
+    """PS item: offsets and limits arrive in AGPRs (%[...] "a" operands) and are copied to
+    scratch VGPRs where used; -inf is a literal; temps come from buffers dead at that point"""
+    qv = (62, 63)                        # Q row offsets (S buffer A, before the first QK^T)
+    out = ["s_waitcnt lgkmcnt(0)", "s_nop 1",
+           f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{NM + 1}, 0",
+           f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LRUN + 1}, 0",
+           f"v_accvgpr_read_b32 v{LIM}, %[lim0]", f"v_accvgpr_read_b32 v{LIM + 1}, %[lim1]",
+           f"v_accvgpr_read_b32 v{qv[0]}, %[qoff0]", f"v_accvgpr_read_b32 v{qv[1]}, %[qoff1]",
+           "s_nop 1"]
+    for rb in (0, 1):
+        for st in range(8):
+            out.append(f"buffer_load_dwordx4 {qtup(rb, st)}, v{qv[rb]}, %[qsrd], 0 offen offset:{32 * st}")
+    for i in range(128):
+        out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
+    out += [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
+    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
+    out += ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
+    out += q_prescale(dt)
+    out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(dt, 2, QK, False, use_nm=False)
+    # reference max of tile 0 (S in buffer A, already in log2 units), masked; then m is
+    # subtracted from tile 0 and set as the C operand of every later QK^T chain
+    out += ["s_nop 7", "s_nop 7", "s_nop 3"]
+    mx, t2, ninf = f"v{PBASE[1] + 24}", f"v{PBASE[1] + 25}", f"v{PBASE[1] + 26}"
+    out.append(f"v_mov_b32 {ninf}, 0xff800000")
+    for rb in (0, 1):
+        out.append(f"v_mov_b32 {mx}, {ninf}")
+        for vv in range(32):
+            v = rb * 32 + vv
+            _, _, _, off, _ = value_info(v)
+            out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}",
+                    f"v_cndmask_b32 {se(0, v)}, {ninf}, {se(0, v)}, vcc",
+                    f"v_max_f32 {mx}, {mx}, {se(0, v)}"]
+        out += [f"v_mov_b32 {t2}, {mx}", "s_nop 1", f"v_permlane32_swap_b32 {mx}, {t2}",
+                "s_nop 1",
+                f"v_max_f32 {mx}, {mx}, {t2}",
+                f"v_sub_f32 {t2}, 0, {mx}",
+                f"v_cmp_lg_f32 vcc, {ninf}, {mx}",
+                f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
+        out += [f"v_add_f32 {se(0, rb * 32 + vv)}, {se(0, rb * 32 + vv)}, v{NM + rb}" for vv in range(32)]
+        out += [f"v_mov_b32 v{NMB + 16 * rb + i}, v{NM + rb}" for i in range(16)]
+    out.append("s_nop 4")
+    out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(dt, 3, QK | SM, False)
+    out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
+    out += main_loop(dt, uid)
+    out += redo_block_ps(dt, 0, uid) + redo_block_ps(dt, 1, uid)
+    out += epilogue(dt, uid)
+    return out
+
+
 def clobbers():
-    regs = [f'"v{i}"' for i in range(216)] + [f'"a{i}"' for i in range(256)]
+    # PS: a[208:239] stay free for the AGPR operands (and the compiler's VGPR spills)
+    agprs = [i for i in range(256) if not (PS and 208 <= i < 240)]
+    regs = [f'"v{i}"' for i in range(NVFIX)] + [f'"a{i}"' for i in agprs]
     regs += [f'"s{i}"' for i in range(SKR, SCM + 2)]
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 
@@ -491,6 +669,13 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[loff0] "v"(loff0)', '[loff1] "v"(loff1)']
 
 
+def ops():
+    if not PS:
+        return OPS
+    av = ("lim0", "lim1", "qoff0", "qoff1", "ooff0", "ooff1", "loff0", "loff1")
+    return [o.replace('"v"', '"a"') if o.split("]")[0][1:] in av else o for o in OPS]
+
+
 def emit():
     lines = [
         "// GENERATED by tools/gen_fwd4.py -- do not edit by hand.",
@@ -504,13 +689,13 @@ def emit():
         "",
     ]
     for dt in ("bf16", "f16"):
-        prog = item_program(dt)
+        prog = item_program_ps(dt) if PS else item_program(dt)
         lines.append(f"__device__ __forceinline__ void fwd4_item_{dt}({SIG}) {{")
         lines.append("    asm volatile(")
         for b in prog:
             lines.append(f'        "{b}\\n"')
         lines.append("        :")
-        lines.append("        : " + ",\n          ".join(OPS))
+        lines.append("        : " + ",\n          ".join(ops()))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
         lines.append("")
@@ -520,4 +705,6 @@ def emit():
 
 
 if __name__ == "__main__":
+    import sys
+    set_mode("--ps" in sys.argv)
     emit()

@@ -22,7 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
-    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwd_fp8"])
+    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwd_fp8", "decode"])
+    ap.add_argument("--ragged", action="store_true", help="decode: cache lengths U[1, 32768]")
+    ap.add_argument("--bf16cache", action="store_true", help="decode: bf16 K/V cache instead of fp8")
     ap.add_argument("--opt", action="append", default=[])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
@@ -68,8 +70,29 @@ def main():
 
     if a.mode == "fwd_fp8":
         q8, k8, v8 = (t.to(torch.float8_e4m3fn) for t in (q, k, v))
+    if a.mode == "decode":
+        # C5 per GPU: B 8, H 32, Hk 8, cache 32768 (fp8 e4m3fn, page 16, random block table)
+        DB, DH, DHK, DS, page = 8, 32, 8, 32768, 16
+        nb = DB * DS // page
+        table = torch.randperm(nb, device="cuda").to(torch.int32).view(DB, DS // page)
+        dq_ = torch.randn(DB, 1, DH, 128, device="cuda", dtype=dt)
+        do_ = torch.empty_like(dq_)
+        dlse = torch.empty(DB, DH, 1, device="cuda", dtype=torch.float32)
+        lens = torch.full((DB,), DS, dtype=torch.int32, device="cuda")
+        if a.ragged:
+            lens = torch.randint(1, DS + 1, (DB,), generator=torch.Generator().manual_seed(0)).to(torch.int32).cuda()
+        kvt = dt if a.bf16cache else torch.float8_e4m3fn
+        kc = (torch.randn(nb, page, DHK, 128, device="cuda") * 4).to(kvt)
+        vc = (torch.randn(nb, page, DHK, 128, device="cuda") * 4).to(kvt)
+        o = do_
+        dbytes = 2 * int(lens.sum()) * DHK * 128 * kc.element_size()
 
     def run(lib):
+        if a.mode == "decode":
+            lib.fmha_page_kvcache_fwd_ex(P(dq_), P(kc), P(vc), P(do_), P(dlse), P(table), DS // page,
+                                         P(lens), 1, DS, DB, DH, DHK, 128, page, 128 ** -0.5, -1, 0,
+                                         0.0, None, 0, 0, 0 if a.bf16cache else 1, 1.0, 1.0, None, False, stream)
+            return
         if a.mode == "fwd_fp8":
             lib.fmha_fwd_fp8(P(q8), P(k8), P(v8), P(o), P(lse), 1.0, 1.0, 1.0, a.s, a.s, a.b, a.h,
                              hk, a.d, sc, -1, wr, False, stream)
@@ -128,8 +151,8 @@ def main():
             times[i].append(s0.elapsed_time(s1) / a.iters)
     for i, p in enumerate(a.libs):
         med = statistics.median(times[i])
-        print(f"{a.mode} {os.path.basename(p)}: median {med:.4f} ms  min {min(times[i]):.4f}"
-              f"  -> {fl / med / 1e9:.1f} TFLOP/s")
+        rate = (f"{dbytes / med / 1e9:.3f} TB/s" if a.mode == "decode" else f"{fl / med / 1e9:.1f} TFLOP/s")
+        print(f"{a.mode} {os.path.basename(p)}: median {med:.4f} ms  min {min(times[i]):.4f}  -> {rate}")
 
 
 if __name__ == "__main__":

@@ -54,6 +54,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // a load whose offset is past `bytes` returns zeros — used instead of `ok ? load : 0`
 // selects, which hipcc lowers to a branch + vmcnt(0) drain per load.
 constexpr int kOOB = 0x7FFFFF00;
+// a wave-uniform pointer pinned to SGPRs (a buffer descriptor built from a base the compiler
+// keeps in VGPRs turns its loads into waterfall loops)
+__device__ __forceinline__ const char* uniform_ptr(const char* ptr) {
+    const uint64_t a = (uint64_t)ptr;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }

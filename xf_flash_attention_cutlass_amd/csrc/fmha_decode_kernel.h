@@ -240,6 +240,8 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
         kpool += (int64_t)bidx * p.k_batch * ESZ;
         vpool += (int64_t)bidx * p.v_batch * ESZ;
     }
+    kpool = uniform_ptr(kpool);
+    vpool = uniform_ptr(vpool);
     const int krow_b = (int)p.k_row * ESZ, vrow_b = (int)p.v_row * ESZ;
     // Page-table entries are wave-uniform per (tile, page): a 32-key tile spans at most two
     // pages, so they are scalar loads through the constant address space (lgkm-counted: they
@@ -275,8 +277,10 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
                 const bool nxt = x >= p.page_size;
                 const int page = __builtin_amdgcn_readfirstlane(nxt ? pg[1] : pg[0]);
                 x = nxt ? x - p.page_size : x;
-                const __amdgpu_buffer_rsrc_t krs = make_rsrc(kpool + (int64_t)page * p.k_batch * ESZ, page_k);
-                const __amdgpu_buffer_rsrc_t vrs = make_rsrc(vpool + (int64_t)page * p.v_batch * ESZ, page_v);
+                // the page base through readfirstlane: computed with a VALU 64-bit multiply-add,
+                // a base left in VGPRs made every load a (single-trip) waterfall loop
+                const __amdgpu_buffer_rsrc_t krs = make_rsrc(uniform_ptr(kpool + (int64_t)page * p.k_batch * ESZ), page_k);
+                const __amdgpu_buffer_rsrc_t vrs = make_rsrc(uniform_ptr(vpool + (int64_t)page * p.v_batch * ESZ), page_v);
                 kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_k, x * krow_b, 0);
                 vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_v, x * vrow_b, 0);
             }
@@ -394,21 +398,41 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
             return MR == 32 ? 4 * hh + (r & 3) + 8 * (r >> 2) : 16 * kb + 4 * hh + r;
         };
         const int keyb = t * kDecKeys;
+        // Softcap / ALiBi and the window edge behind wave-uniform branches: written as per-score
+        // conditions, the compiler if-converted them and ran tanh (exp + rcp) and the ALiBi
+        // distance on every score of every tile
         const bool edge = (t + 1) * kDecKeys > min(sk, my_lr) || t * kDecKeys < my_ll;
+        if (KV8) {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int r = 0; r < NA; ++r) st[kb][r] *= p.k_scale;
+        }
+        if (p.softcap_pre > 0.f || p.alibi) {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int r = 0; r < NA; ++r) {
+                    float x = st[kb][r];
+                    if (p.softcap_pre > 0.f) x = fast_tanh(x * p.softcap_pre);
+                    if (p.alibi) x -= alibi_w * (float)abs(pos + diag - (keyb + keyof(kb, r)));
+                    st[kb][r] = x;
+                }
+        }
+        if (__builtin_amdgcn_ballot_w64(edge)) {
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int r = 0; r < NA; ++r) {
+                    const int key = keyb + keyof(kb, r);
+                    if (edge && (key >= my_lr || key < my_ll)) st[kb][r] = -INFINITY;
+                }
+        }
         float mx = -INFINITY;
 #pragma unroll
         for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-            for (int r = 0; r < NA; ++r) {
-                float x = st[kb][r];
-                if (KV8) x *= p.k_scale;
-                if (p.softcap_pre > 0.f) x = fast_tanh(x * p.softcap_pre);
-                const int key = keyb + keyof(kb, r);
-                if (p.alibi) x -= alibi_w * (float)abs(pos + diag - key);
-                if (edge && (key >= my_lr || key < my_ll)) x = -INFINITY;
-                st[kb][r] = x;
-                mx = fmaxf(mx, x);
-            }
+            for (int r = 0; r < NA; ++r) mx = fmaxf(mx, st[kb][r]);
         mx = MR == 32 ? wave_max_halves(mx) : quad_max16(mx);
         const float m_new = fmaxf(m_run, mx);
         const float mref = (m_new == -INFINITY) ? 0.f : m_new * c;
