@@ -62,8 +62,11 @@ __device__ __forceinline__ const char* uniform_ptr(const char* ptr) {
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
 }
+// (every descriptor here covers a wave-uniform range: base and size are pinned to SGPRs, a
+// no-op where the compiler already has them there)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(uniform_ptr(reinterpret_cast<const char*>(base))),
+                                             (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
 __device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);

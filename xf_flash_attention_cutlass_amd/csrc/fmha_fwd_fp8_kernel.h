@@ -461,7 +461,7 @@ __device__ __forceinline__ void fwd8_item(const FwdParams& p, char* smem, const 
         // fmha_fwd_kernel.h: a wave stops after the last tile any of its rows sees, drains it,
         // then keeps only its DMA share and the barriers (bit-identical results)
         const int t_w = __builtin_amdgcn_readfirstlane((w_lr_max + kBlockN - 1) / kBlockN - 1);
-        const int nsteps_w = wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps;
+        const int nsteps_w = __builtin_amdgcn_readfirstlane(wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps);
         int r = 0;
         while (r < nsteps_w) {
             step(I1{}, I0{}, I3{}, lo + r, sa, sb);

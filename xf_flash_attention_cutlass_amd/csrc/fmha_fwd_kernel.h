@@ -466,7 +466,10 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     }
     typedef __attribute__((address_space(3))) void lds_void;
     auto dma_tile = [&](const int nb, const int buf) {
-        const int kso = nb * kBlockN * (int)p.k_row * 2, vso = nb * kBlockN * (int)p.v_row * 2;
+        // (soffset pinned to an SGPR: derived from a tile index the compiler kept in a VGPR,
+        // each DMA piece became a waterfall loop)
+        const int kso = __builtin_amdgcn_readfirstlane(nb * kBlockN * (int)p.k_row * 2);
+        const int vso = __builtin_amdgcn_readfirstlane(nb * kBlockN * (int)p.v_row * 2);
 #pragma unroll
         for (int i = 0; i < IPW; ++i) {
             const int g = wave_u * IPW + i;
@@ -636,7 +639,7 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
         // The skipped tiles would add exact zeros, so results are bit-identical, and the
         // wave's SIMD partner gets the whole issue port meanwhile.
         const int t_w = __builtin_amdgcn_readfirstlane((w_lr_max + kBlockN - 1) / kBlockN - 1);
-        const int nsteps_w = wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps;
+        const int nsteps_w = __builtin_amdgcn_readfirstlane(wave_ok ? max(0, min(nsteps, t_w - lo)) : nsteps);
         int r = 0;
         while (r < nsteps_w) {
             step(I1{}, I0{}, I3{}, lo + r, sa, sb);
