@@ -302,9 +302,19 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         {
             const int pos = (t_lo + tt) * BQ + lr;
             const bool ok = pos < sq;
-            const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off +
-                               (ok ? pos : 0);
-            lsd_raw = (hh ? p.dsum : p.lse)[li];
+            const int64_t lrow = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off;
+            if constexpr (MASK) {
+                // both rows through wave-uniform descriptors and a select: in the masked
+                // instances the per-lane pointer select (hh ? dsum : lse) was a 64-bit VGPR the
+                // allocator spilled, and its scratch reload's vmcnt(0) retired the previous
+                // tile's dQ atomics at every iteration start (C3 +0.8 %)
+                const int off = (ok ? pos : 0) * 4;
+                const float l = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.lse + lrow, (uint32_t)(sq * 4)), off, 0, 0));
+                const float d = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.dsum + lrow, (uint32_t)(sq * 4)), off, 0, 0));
+                lsd_raw = hh ? d : l;
+            } else {
+                lsd_raw = (hh ? p.dsum : p.lse)[lrow + (ok ? pos : 0)];
+            }
             lsd_ok = ok;
         }
         // buffer loads over this head's rows [q0, sq): rows past the end and padded head-dim
@@ -489,11 +499,8 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                     if (FEAT && p.softcap_on) { w = fast_tanh(w * p.softcap_pre); dcap = 1.f - w * w; }
                     if (FEAT && p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
                     float pr = fast_exp2(fmaf(w, c, -lse4[i]));
-                    if (need_mask) {
-                        // visible keys of row pos: [lo, hi) -> one unsigned compare
-                        const int hi = (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk;
-                        const int lo = (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0;
-                        pr = (unsigned)(key - lo) < (unsigned)max(hi - lo, 0) ? pr : 0.f;
+                    if (!MASK && need_mask) {   // (unmasked instances: keys past the end only)
+                        pr = (unsigned)key < (unsigned)max(sk, 0) ? pr : 0.f;
                     }
                     if (FEAT && p.drop) {
                         const bool keep = drop_keep(dw[i], key & 3, p.keep_thr);
@@ -505,6 +512,26 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                     }
                 }
             }
+        }
+        // masked instances: the window / key-range mask as one wave-uniform block after the tile
+        // (inside the unrolled score loop the compiler split the tile into a branch per score;
+        // C3 +2.4 %): P and dS of invisible scores -> 0
+        if (MASK && need_mask) {
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * gq + i;
+                        const int pos = q0 + 8 * gq + 4 * hh + i;
+                        // visible keys of row pos: [lo, hi) -> one unsigned compare
+                        const int hi = (MASK && p.wr >= 0) ? min(sk, pos + diag + p.wr + 1) : sk;
+                        const int lo = (MASK && p.wl >= 0) ? max(0, pos + diag - p.wl) : 0;
+                        const bool vis = (unsigned)(my_key[ks] - lo) < (unsigned)max(hi - lo, 0);
+                        s_acc[ks][r] = vis ? s_acc[ks][r] : 0.f;
+                        dp_acc[ks][r] = vis ? dp_acc[ks][r] : 0.f;
+                    }
         }
         // ---- dV^T += dO^T P ; dK^T += Q^T dS  (P / dS accumulators are the B operands)
 #pragma unroll
