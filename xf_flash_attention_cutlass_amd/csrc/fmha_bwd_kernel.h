@@ -361,6 +361,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     auto kaddr = [&](const int s) { return kaddr_[s % NA] + (s / NA) * 256; };
     auto qaddr = [&](const int s) { return qaddr_[s % NA] + (s / NA) * 256; };
     const int q4 = (lane & 15) >> 2;
+    // LDS addresses as integers that include the LDS base of their tile, so every constant part
+    // (ring row block, d tile, key subtile, dO vs Q) lands in the ds_read offset field (from a
+    // pointer into smem the compiler added an SGPR base to the lane offset before every read)
+    const int sbase = (int)(size_t)smem;
+    constexpr int Q_OFF = (VR ? 1 : 2) * KT_BYTES, DS_OFF = Q_OFF + 2 * QT_BYTES;
     int troff_[2][NTA];   // transposed reads of the Q / dO tile (A operand: rows q, column d)
 #pragma unroll
     for (int part = 0; part < 2; ++part)
@@ -368,7 +373,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < NTA; ++dt) {
             const int r = 4 * hh + q4 + 8 * part;
             const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-            troff_[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+            troff_[part][dt] = sbase + Q_OFF + lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
         }
     auto troff = [&](const int part, const int dt) { return troff_[part][dt % NTA] + (dt / NTA) * 256; };
     // dQ phase (16x16x32): wave -> query half mt, d tiles
@@ -382,11 +387,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
         const int kr0 = 8 * g16 + qq + 4 * part;
-        dq_aoff[part] = ds_off(kr0, 16 * mt + 4 * p4);
+        dq_aoff[part] = sbase + DS_OFF + ds_off(kr0, 16 * mt + 4 * p4);
 #pragma unroll
         for (int i = 0; i < (HD > 128 ? 1 : NDQ); ++i) {
             const int dcol = 16 * ((wave >> 1) * NDQ + i) + 4 * p4;
-            dq_boff[i][part] = lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
+            dq_boff[i][part] = sbase + lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
         }
     }
 
@@ -395,7 +400,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         if constexpr (HD > 128) {
             const int kr0 = 8 * g16 + qq + 4 * part;
             const int dcol = 16 * ((wave >> 1) * NDQ + i) + 4 * p4;
-            return lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
+            return sbase + lds_off<HD>(kr0, dcol >> 3) + 8 * ((dcol >> 2) & 1);
         } else {
             return dq_boff[i][part];
         }
@@ -539,11 +544,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             const int rb = 16 * sp * HD * 2;
 #pragma unroll
             for (int dt = 0; dt < ND; ++dt) {
-                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff(0, dt)));
-                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(do_lds + rb + troff(1, dt)));
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(troff(0, dt) + QT_BYTES + rb));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(troff(1, dt) + QT_BYTES + rb));
                 const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff(0, dt)));
-                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(q_lds + rb + troff(1, dt)));
+                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(troff(0, dt) + rb));
+                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(troff(1, dt) + rb));
                 const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
 #pragma unroll
                 for (int ks = 0; ks < KS; ++ks) {
@@ -582,16 +587,16 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             for (int i = 0; i < NDQ; ++i) dq[i] = f32x4{};
 #pragma unroll
             for (int ks = 0; ks < BN / 32; ++ks) {
-                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 32 * 64 + dq_aoff[0]));
-                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ds_lds + ks * 32 * 64 + dq_aoff[1]));
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(dq_aoff[0] + ks * 32 * 64));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(dq_aoff[1] + ks * 32 * 64));
                 const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
                 const V8 a = __builtin_bit_cast(V8, av);
 #pragma unroll
                 for (int i = 0; i < NDQ; ++i) {
                     const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dqb(i, 0)));
+                        (lds_s16x4*)(size_t)(dqb(i, 0) + ks * 32 * HD * 2));
                     const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(k_lds + ks * 32 * HD * 2 + dqb(i, 1)));
+                        (lds_s16x4*)(size_t)(dqb(i, 1) + ks * 32 * HD * 2));
                     const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                     dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
                 }
