@@ -292,9 +292,12 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     // The raw value is kept until the end of the iteration: converting it right after the
     // load makes the wave wait vmcnt on it, and vmcnt is in order, so that wait would also
     // retire the previous tile's dQ atomics (thousands of cycles with every CU issuing).
-    float lsd_raw = 0.f;
+    float lsd_raw = 0.f, lsd_raw2 = 0.f;   // (masked instances: LSE in lsd_raw, D in lsd_raw2)
     bool lsd_ok = false;
-    auto lsd_value = [&]() { return hh ? (lsd_ok ? lsd_raw : 0.f) : (lsd_ok ? lsd_raw * kLog2e : INFINITY); };
+    auto lsd_value = [&]() {
+        const float dv = MASK ? lsd_raw2 : lsd_raw;
+        return hh ? (lsd_ok ? dv : 0.f) : (lsd_ok ? lsd_raw * kLog2e : INFINITY);
+    };
     auto load_q = [&](int it) {
         const int g = it / ntiles;
         const int tt = p.desc ? (g + 1) * ntiles - 1 - it : it - g * ntiles;
@@ -308,10 +311,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 // instances the per-lane pointer select (hh ? dsum : lse) was a 64-bit VGPR the
                 // allocator spilled, and its scratch reload's vmcnt(0) retired the previous
                 // tile's dQ atomics at every iteration start (C3 +0.8 %)
+                // (both kept raw until lsd_value(): selecting right after the loads waits for
+                // them there, and vmcnt being in order, for every older memory op too)
                 const int off = (ok ? pos : 0) * 4;
-                const float l = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.lse + lrow, (uint32_t)(sq * 4)), off, 0, 0));
-                const float d = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.dsum + lrow, (uint32_t)(sq * 4)), off, 0, 0));
-                lsd_raw = hh ? d : l;
+                lsd_raw = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.lse + lrow, (uint32_t)(sq * 4)), off, 0, 0));
+                lsd_raw2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.dsum + lrow, (uint32_t)(sq * 4)), off, 0, 0));
             } else {
                 lsd_raw = (hh ? p.dsum : p.lse)[lrow + (ok ? pos : 0)];
             }
@@ -431,7 +435,11 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         // barrier), read back below as broadcast float4s
         const float lsd = lsd_cur;
         if constexpr (LSD != kLsdPermute) lsd_slot[lane] = lsd;
-        if (!VR && it + 1 < n_iter) load_q(it + 1);
+        // (!VR: unconditional — the last iteration reloads its own tile — so the compiler's
+        // waitcnt analysis sees the loads and their wait on every path; conditional, it kept
+        // them pending across the back-edge and waited vmcnt at the loop head, retiring the
+        // previous tile's dQ atomics there)
+        if (!VR) load_q(min(it + 1, n_iter - 1));
 
         // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
         f32x16 s_acc[KS], dp_acc[KS];
@@ -577,7 +585,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         }
         __syncthreads();
         // Q / dO of this tile are dead after the barrier above (dQ reads only dS^T and K)
-        if (it + 1 < n_iter) store_q();
+        if (!VR || it + 1 < n_iter) store_q();
         lsd_cur = lsd_value();      // every vmcnt wait of the iteration comes before its atomics
         asm volatile("" : "+v"(lsd_cur));   // (pinned: not sunk below the atomics)
         // ---- dQ[q][d] += dS K over the 256 keys (16x16x32; A = dS via tr-read of dS^T)
