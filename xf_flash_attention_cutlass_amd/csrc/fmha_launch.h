@@ -37,8 +37,9 @@ struct Options {
     std::atomic<int> bwd_order{0};       // backward grid: 1 = the key blocks of one (b, kv head) consecutive
                                          // on one XCD (they then sweep the same Q / dO tiles together;
                                          // C3: 3.03 vs 2.88 ms - their dQ atomics then collide)
-    std::atomic<int> bwd_desc{0};        // backward query-tile sweep: 1 = last tile first (C3: 2.86 vs
-                                         // 2.88 ms, within noise)
+    std::atomic<int> bwd_desc{1};        // backward query-tile sweep: 1 = last tile first (C3 on the
+                                         // round-3 session-2 kernel: 2.496 vs 2.513 ms, non-causal
+                                         // 4.410 vs 4.423; dK/dV equal up to fp32 summation order)
     std::atomic<int> dec_hmaj{1};        // decode workgroup: 0 = 1 kv head x 4 splits, 1 = 4 kv heads x one
                                          // split, 2 = 8 kv heads x one split (C5 fp8: 116 / 110 / 112 us)
 };
