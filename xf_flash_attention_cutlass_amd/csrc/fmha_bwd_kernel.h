@@ -307,12 +307,10 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
             const bool ok = pos < sq;
             const int64_t lrow = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off;
             if constexpr (MASK) {
-                // both rows through wave-uniform descriptors and a select: in the masked
-                // instances the per-lane pointer select (hh ? dsum : lse) was a 64-bit VGPR the
-                // allocator spilled, and its scratch reload's vmcnt(0) retired the previous
-                // tile's dQ atomics at every iteration start (C3 +0.8 %)
-                // (both kept raw until lsd_value(): selecting right after the loads waits for
-                // them there, and vmcnt being in order, for every older memory op too)
+                // both rows load through wave-uniform descriptors and stay raw until
+                // lsd_value() picks one. A per-lane pointer select (hh ? dsum : lse) here is a
+                // 64-bit VGPR the allocator spills in these instances; the scratch reload's
+                // vmcnt(0) then retires the previous tile's dQ atomics every iteration (C3 +0.8 %)
                 const int off = (ok ? pos : 0) * 4;
                 lsd_raw = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.lse + lrow, (uint32_t)(sq * 4)), off, 0, 0));
                 lsd_raw2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(p.dsum + lrow, (uint32_t)(sq * 4)), off, 0, 0));
