@@ -25,6 +25,16 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* ABI 2.1: the entries whose argument lists changed in 2.0 are exported under _v2 names; these
+ * macros keep sources that call the plain names compiling unchanged, while a binary built
+ * against the 1.0 header fails to link instead of calling them with a stale argument list
+ * (the pattern of the CUDA driver API's cuMemAlloc -> cuMemAlloc_v2). */
+#define fmha_varlen_fwd_ex fmha_varlen_fwd_ex_v2
+#define fmha_page_kvcache_fwd_ex fmha_page_kvcache_fwd_ex_v2
+#define fmha_bwd_workspace_size fmha_bwd_workspace_size_v2
+#define fmha_varlen_bwd_workspace_size fmha_varlen_bwd_workspace_size_v2
+#define fmha_varlen_bwd fmha_varlen_bwd_v2
+
 #ifdef __cplusplus
 #define FMHA_DEFAULT(x) = x
 extern "C" {
@@ -97,8 +107,9 @@ int fmha_last_num_splits(void);
  * scores with the same state drop the same entries (flash-attn's rng_state = {seed, offset}). */
 void fmha_set_rng_state(uint64_t seed, uint64_t offset);
 
-/* Library version / build identification, e.g. "xf-fmha-gfx950 2.0".  2.0 (round 3) changed
- * argument lists of existing symbols (see INTEGRATION.md "ABI history"). */
+/* Library version / build identification, e.g. "xf-fmha-gfx950 2.1".  2.0 (round 3) changed
+ * argument lists of existing symbols; 2.1 exports those under _v2 names (see INTEGRATION.md
+ * "ABI history"). */
 const char* fmha_version(void);
 
 /* Process-wide schedule knobs; every setting computes the same results (the parity suite runs
@@ -147,7 +158,7 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
  * [num_blocks, page, heads_k, head_size], block_table [batch, block_table_stride]).
  * p_dropout / s_dmask: as fmha_fwd (non-paged only; s_dmask [batch, heads,
  * round128(max_seqlen_q), round128(max_seqlen_k)], each sequence's rows from 0). */
-void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
+void fmha_varlen_fwd_ex_v2(void* q, void* k, void* v, void* o, void* softmax_lse,
                         void* cu_seqlens_q, void* cu_seqlens_k, void* seqused_k,
                         void* block_table, int32_t block_table_stride, int32_t page_block_size,
                         void* alibi_slopes, int32_t alibi_batch_stride,
@@ -165,7 +176,7 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
  * out in export.cpp:1627-1634): batch b attends over cache rows [cache_leftpad[b],
  * cache_seqlens[b]), key positions counted from cache_leftpad[b].  Only for one page per
  * sequence (max_seqlen_k <= page_block_size), as the reference: no paged KV with leftpad. */
-void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
+void fmha_page_kvcache_fwd_ex_v2(void* q, void* kcache, void* vcache, void* o, void* softmax_lse,
                               void* block_table, int32_t block_table_stride, void* cache_seqlens,
                               int32_t seqlen_q, int32_t max_seqlen_k, int32_t batch_size,
                               int32_t num_heads, int32_t num_heads_k, int32_t head_size,
@@ -217,7 +228,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
               int window_size_left, int window_size_right, float softcap, bool deterministic,
               bool is_fp16, hipStream_t stream, void* workspace, size_t workspace_bytes);
 
-size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
+size_t fmha_bwd_workspace_size_v2(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
                                int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                bool deterministic);
 
@@ -226,7 +237,7 @@ size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch
  * [num_heads, total_q] receives rowsum(dO*O) (may be NULL: pool scratch).  deterministic and
  * workspace as fmha_bwd (fmha_varlen_bwd_workspace_size(..., deterministic) bytes); p_dropout as
  * fmha_bwd. */
-void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
+void fmha_varlen_bwd_v2(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
                      void* dq, void* dk, void* dv, void* cu_seqlens_q, void* cu_seqlens_k,
                      void* alibi_slopes, int32_t alibi_batch_stride, int32_t max_seqlen_q,
                      int32_t max_seqlen_k, int32_t total_q, int32_t total_k,
@@ -236,7 +247,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
                      hipStream_t stream, void* workspace, size_t workspace_bytes,
                      void* softmax_d, float p_dropout);
 
-size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t batch_size,
+size_t fmha_varlen_bwd_workspace_size_v2(int32_t total_q, int32_t max_seqlen_k, int32_t batch_size,
                                       int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                       bool deterministic);
 

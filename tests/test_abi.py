@@ -56,7 +56,7 @@ def test_version():
 
 
 def _fwd(**over):
-    a = dict(q=1, k=1, v=1, o=1, alibi=None, sq=16, sk=16, b=1, h=4, hk=2, d=64, p=0.0,
+    a = dict(q=16, k=16, v=16, o=16, alibi=None, sq=16, sk=16, b=1, h=4, hk=2, d=64, p=0.0,
              stream=None, dprops=None, scale=0.125, p_ptr=None, lse=None, wl=-1, wr=-1,
              softcap=0.0, ret=False, fp16=False, splits=1)
     a.update(over)
@@ -86,7 +86,7 @@ def test_error_state_is_cleared_by_next_call():
     status, _ = _fwd(b=0)
     assert status != 0
     L = capi.lib()
-    L.fmha_page_kvcache_fwd(1, 1, 1, None, None, 1, None, None, 64, 1, 64, 1, 4, 4, 64, 16,
+    L.fmha_page_kvcache_fwd(16, 16, 16, None, None, 16, None, None, 64, 1, 64, 1, 4, 4, 64, 16,
                             None, 0.125, -1, -1, 1, None, None, None, False, False, False)
     # missing block table is a validation error, reported with a new message
     assert L.fmha_last_status() != 0 and "block_table" in L.fmha_last_error().decode()

@@ -145,11 +145,15 @@ def test_bwd_capi_workspace_and_errors(xfa):
     capi.check()
     L.fmha_bwd(*args, ws.data_ptr(), 16)
     assert L.fmha_last_status() != 0 and "workspace" in L.fmha_last_error().decode()
-    # deterministic: one dq_accum slice per 256-key block (a single block here)
-    assert L.fmha_bwd_workspace_size(s, s, b, h, h, d, True) == ws_n
+    # deterministic: ceil(CUs / (b * hk)) dq_accum slices, whatever seqlen_k is
+    ws_d = L.fmha_bwd_workspace_size(s, s, b, h, h, d, True)
+    assert ws_d == L.fmha_bwd_workspace_size(s, 1000, b, h, h, d, True) > ws_n
     args_det = list(args)
     args_det[22] = True
     L.fmha_bwd(*args_det, ws.data_ptr(), ws_n)
+    assert L.fmha_last_status() != 0 and "workspace" in L.fmha_last_error().decode()
+    wsd = torch.empty(ws_d, device=DEV, dtype=torch.uint8)
+    L.fmha_bwd(*args_det, wsd.data_ptr(), ws_d)
     capi.check()
 
 
@@ -161,9 +165,10 @@ def _run_det(xfa, q, k, v, g, **kw):
 @pytest.mark.parametrize("causal,window", [(False, (-1, -1)), (True, (-1, -1)), (False, (100, 30))])
 @pytest.mark.parametrize("sq,sk,h,hk", [(700, 700, 4, 2), (300, 1100, 2, 1)])
 def test_bwd_deterministic(xfa, d, causal, window, sq, sk, h, hk):
-    """deterministic=True (export.cpp:1086-1092 semantics): dQ partials per key block are summed
-    in key-block order, so two runs agree bit for bit; the gradients meet the oracle rule and
-    equal the atomic path's to fp32 reassociation."""
+    """deterministic=True (export.cpp:1086-1092 semantics): dQ partials are added into
+    ceil(CUs / (b * hk)) slices in key-block order and the slices summed in order, so two runs
+    agree bit for bit; the gradients meet the oracle rule and equal the atomic path's to fp32
+    reassociation."""
     gen = torch.Generator().manual_seed(11)
     q = torch.randn(2, sq, h, d, generator=gen).bfloat16()
     k = torch.randn(2, sk, hk, d, generator=gen).bfloat16()
@@ -180,6 +185,60 @@ def test_bwd_deterministic(xfa, d, causal, window, sq, sk, h, hk):
     ref, pt = _oracle_grads(q, k, v, g, causal=causal, window_size=w)
     for nm, x, r, p in zip(("dq", "dk", "dv"), a, ref, pt):
         _grad_check(f"det {nm} {sq}x{sk} d{d} c{causal} w{window}", x, r, p)
+
+
+@pytest.mark.parametrize("b,h,hk,s,d,causal", [(8, 32, 32, 1024, 128, True),
+                                                (8, 32, 32, 1024, 128, False),
+                                                (4, 64, 8, 4096, 128, True),
+                                                (16, 16, 16, 1024, 64, True),
+                                                (8, 32, 32, 640, 256, False)])
+def test_bwd_deterministic_walk(xfa, b, h, hk, s, d, causal):
+    """Shapes with fewer dQ slices than key blocks (b * hk >= 32): each workgroup walks several
+    key blocks into its slice.  Bitwise reproducible, dK/dV equal to the atomic path, dQ within
+    fp32 reassociation of it, sampled (batch, head) gradients against the oracle."""
+    gen = torch.Generator(device=DEV).manual_seed(13)
+    q = torch.randn(b, s, h, d, device=DEV, generator=gen).bfloat16()
+    k = torch.randn(b, s, hk, d, device=DEV, generator=gen).bfloat16()
+    v = torch.randn(b, s, hk, d, device=DEV, generator=gen).bfloat16()
+    g = torch.randn(b, s, h, d, device=DEV, generator=gen).bfloat16()
+    a = _run_det(xfa, q, k, v, g, causal=causal)
+    b_ = _run_det(xfa, q, k, v, g, causal=causal)
+    for x, y in zip(a, b_):
+        assert torch.equal(x, y)
+    nondet = _run(xfa, q, k, v, g, causal=causal)
+    assert torch.equal(a[1], nondet[1]) and torch.equal(a[2], nondet[2])
+    assert (a[0].float() - nondet[0].float()).abs().max().item() < 2e-2
+    G = h // hk
+    for bi, hi in ((0, 0), (b - 1, h - 1)):
+        kh = hi // G
+        sl = [x[bi:bi + 1, :, hi:hi + 1].cpu() for x in (q, g)]
+        ks, vs = (x[bi:bi + 1, :, kh:kh + 1].cpu() for x in (k, v))
+        ref, pt = _oracle_grads(sl[0], ks, vs, sl[1], causal=causal)
+        # dK / dV of kv head kh sum over its G query heads: only dQ is per query head; for
+        # G = 1 all three are checked
+        names = ("dq", "dk", "dv") if G == 1 else ("dq",)
+        got = (a[0][bi:bi + 1, :, hi:hi + 1], a[1][bi:bi + 1, :, kh:kh + 1],
+               a[2][bi:bi + 1, :, kh:kh + 1])
+        for nm, x, r, p in zip(names, got, ref, pt):
+            _grad_check(f"det walk {nm} b{bi} h{hi} s{s} d{d} c{causal}", x, r, p)
+
+
+def test_bwd_deterministic_long(xfa):
+    """B4 H32 S16384 D128 causal: 64 key blocks per (batch, head) into 2 slices (the per-key-block
+    scheme of round 3 needed 64 GiB of slices here and refused the call).  Bitwise reproducible,
+    dK/dV equal to the atomic path, dQ within fp32 reassociation."""
+    B, S, H, D = 4, 16384, 32, 128
+    gen = torch.Generator(device=DEV).manual_seed(14)
+    q, k, v, g = (torch.randn(B, S, H, D, device=DEV, generator=gen).bfloat16() for _ in range(4))
+    from xf_flash_attention_cutlass_amd import capi
+    assert capi.lib().fmha_bwd_workspace_size(S, S, B, H, H, D, True) < (3 << 30)
+    a = _run_det(xfa, q, k, v, g, causal=True)
+    b_ = _run_det(xfa, q, k, v, g, causal=True)
+    for x, y in zip(a, b_):
+        assert torch.equal(x, y)
+    nondet = _run(xfa, q, k, v, g, causal=True)
+    assert torch.equal(a[1], nondet[1]) and torch.equal(a[2], nondet[2])
+    assert (a[0].float() - nondet[0].float()).abs().max().item() < 2e-2
 
 
 def test_bwd_deterministic_varlen(xfa):

@@ -1,6 +1,6 @@
 """CPU: host-side guards of the C ABI and the Python wrappers, reached with fake pointers (no
 kernel is launched): the 32-bit slab limit (fmha_api.cpp slab_ok), the deterministic
-backward's workspace bound, and the fp8 wrapper refusing options it cannot honour."""
+backward's workspace size, and the fp8 wrapper refusing options it cannot honour."""
 import pytest
 import torch
 
@@ -59,18 +59,25 @@ def test_varlen_bwd_slab_guard_dq_accum():
     assert st != 0 and "dq_accum" in msg
 
 
-def test_deterministic_bwd_workspace_bound():
-    # b8 h32 s32768 d128: one 1 GiB-per-slice x 128 key blocks -> far above the 32 GiB limit
+def test_deterministic_bwd_workspace_independent_of_seqlen_k():
+    """deterministic=True: S = ceil(CUs / (b * hk)) dQ slices (export.cpp:1090-1091's bound), not
+    one per key block, so the workspace does not grow with seqlen_k (no device here: the library
+    assumes MI355X's 256 CUs)."""
     L = capi.lib()
-    L.fmha_bwd(FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, None, None, 32768, 32768, 8,
-               32, 32, 128, 0.0, 0.088, -1, -1, 0.0, True, False, None, None, 0)
-    st, msg = _status()
-    assert st != 0 and "deterministic" in msg
-    # the same shape without determinism passes validation (the launch itself is not reached:
-    # check only that the bound is what refused it, via the workspace-size query)
-    need = L.fmha_bwd_workspace_size(32768, 32768, 8, 32, 32, 128, True)
-    assert need > (32 << 30)
-    assert L.fmha_bwd_workspace_size(32768, 32768, 8, 32, 32, 128, False) < need
+    acc = lambda tok, h: tok * h * 128 * 4               # noqa: E731  fp32 [tokens][h][128]
+    for b, h, hk, sq in ((4, 32, 32, 16384), (1, 16, 16, 45056), (8, 32, 8, 1024), (1, 1, 1, 4096)):
+        sizes = {sk: L.fmha_bwd_workspace_size(sq, sk, b, h, hk, 128, True)
+                 for sk in (128, 4096, 65536, 1 << 20)}
+        assert len(set(sizes.values())) == 1, sizes
+        slices = -(-256 // (b * hk))
+        dsum = -(-(b * sq * h * 4) // 256) * 256
+        assert sizes[128] == slices * acc(b * sq, h) + dsum
+        assert L.fmha_bwd_workspace_size(sq, 4096, b, h, hk, 128, False) == acc(b * sq, h) + dsum
+        v = {mk: L.fmha_varlen_bwd_workspace_size(b * sq, mk, b, h, hk, 128, True)
+             for mk in (64, 8192, 1 << 19)}
+        assert len(set(v.values())) == 1 and v[64] == sizes[128]
+    # B4 H32 S16384 D128: two slices (the old per-key-block scheme needed 64)
+    assert L.fmha_bwd_workspace_size(16384, 16384, 4, 32, 32, 128, True) < 3 * acc(4 * 16384, 32)
 
 
 @pytest.mark.parametrize("kw", [dict(dropout_p=0.1), dict(softcap=30.0),
@@ -80,3 +87,38 @@ def test_fp8_wrapper_refuses_unsupported_options(kw):
     q = torch.zeros(1, 16, 2, 128, dtype=torch.float8_e4m3fn)
     with pytest.raises(NotImplementedError):
         flash_attn_func(q, q, q, **kw)
+
+
+def test_misaligned_pointers_and_strides_rejected():
+    """The kernels move 16-byte chunks: the C ABI refuses bases that are not 16-byte aligned and
+    (strided entry) strides that are not multiples of 8 elements, instead of faulting."""
+    L = capi.lib()
+    L.fmha_fwd(FAKE + 2, FAKE, FAKE, FAKE, None, 128, 128, 1, 4, 4, 128, 0.0, None, None,
+               0.088, None, None, -1, -1, 0.0, False, False, 1)
+    st, msg = _status()
+    assert st != 0 and "16-byte aligned" in msg
+    L.fmha_bwd(FAKE, FAKE, FAKE, FAKE + 8, FAKE, FAKE, FAKE, FAKE, FAKE, None, None, 128, 128, 1,
+               4, 4, 128, 0.0, 0.088, -1, -1, 0.0, False, False, None, None, 0)
+    st, msg = _status()
+    assert st != 0 and "16-byte aligned" in msg
+    import ctypes
+    strides = (ctypes.c_int64 * 12)(128 * 4 * 128, 4 * 128 + 4, 128, 128 * 4 * 128, 4 * 128, 128,
+                                    128 * 4 * 128, 4 * 128, 128, 128 * 4 * 128, 4 * 128, 128)
+    L.fmha_fwd_strided(FAKE, FAKE, FAKE, FAKE, None, None, 128, 128, 2, 4, 4, 128, strides, 0.088,
+                       -1, -1, 0.0, False, 1, None, 0.0, None)
+    st, msg = _status()
+    assert st != 0 and "multiples of 8 elements" in msg and "stride 1" in msg
+
+
+def test_softcap_with_dropout_rejected():
+    """The reference refuses softcap together with dropout (export.cpp:515,737,
+    flash_api_hip.cpp:400,606,895,1128); so does every C entry that takes both."""
+    L = capi.lib()
+    L.fmha_fwd(FAKE, FAKE, FAKE, FAKE, None, 128, 128, 1, 4, 4, 128, 0.1, None, None, 0.088, None,
+               None, -1, -1, 30.0, False, False, 1)
+    st, msg = _status()
+    assert st != 0 and "Softcapping does not support dropout" in msg
+    L.fmha_bwd(FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, None, None, 128, 128, 1, 4, 4,
+               128, 0.1, 0.088, -1, -1, 30.0, False, False, None, None, 0)
+    st, msg = _status()
+    assert st != 0 and "Softcapping does not support dropout" in msg

@@ -27,18 +27,18 @@ _SIGS = {
                          f32, vp],
     "fmha_fwd_fp8": [vp, vp, vp, vp, vp, f32, f32, f32, i32, i32, i32, i32, i32, i32, f32,
                      C.c_int, C.c_int, b_, vp],
-    "fmha_varlen_fwd_ex": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,
+    "fmha_varlen_fwd_ex_v2": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, i32,
                            i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, vp, f32, vp],
-    "fmha_page_kvcache_fwd_ex": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32,
+    "fmha_page_kvcache_fwd_ex_v2": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, i32,
                                  i32, f32, C.c_int, C.c_int, f32, vp, i32, i32, i32, f32, f32, vp,
                                  b_, vp],
     "fmha_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                  f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz],
-    "fmha_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
-    "fmha_varlen_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
+    "fmha_bwd_workspace_size_v2": [i32, i32, i32, i32, i32, i32, b_],
+    "fmha_varlen_bwd_v2": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                         i32, i32, i32, i32, f32, C.c_int, C.c_int, f32, b_, b_, vp, vp, sz, vp,
                         f32],
-    "fmha_varlen_bwd_workspace_size": [i32, i32, i32, i32, i32, i32, b_],
+    "fmha_varlen_bwd_workspace_size_v2": [i32, i32, i32, i32, i32, i32, b_],
     "fmha_kvcache_append": [vp, vp, vp, vp, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, b_,
                             b_, i32, i32, i32, i32, i32, b_, vp],
     "fmha_last_error": [],
@@ -52,7 +52,7 @@ _SIGS = {
 _RES = {"fmha_last_error": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
         "fmha_last_num_splits": C.c_int,
         "fmha_set_option": C.c_int, "fmha_get_option": C.c_int,
-        "fmha_bwd_workspace_size": sz, "fmha_varlen_bwd_workspace_size": sz}
+        "fmha_bwd_workspace_size_v2": sz, "fmha_varlen_bwd_workspace_size_v2": sz}
 
 EXPORTED = tuple(_SIGS)
 
@@ -65,11 +65,18 @@ def load(path: str = LIB_PATH, strict: bool = True) -> C.CDLL:
                           "xf_flash_attention_cutlass_amd/build.py` (no CPU fallback exists)")
     lib = C.CDLL(path)
     for name, args in _SIGS.items():
-        if not strict and not hasattr(lib, name):
-            continue
+        plain = name[:-3] if name.endswith("_v2") else None
+        if not hasattr(lib, name):
+            if strict:
+                getattr(lib, name)                 # raises: the build lacks a declared symbol
+            if not (plain and hasattr(lib, plain)):
+                continue
+            name = plain                           # an older (2.0) A/B build: plain names
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = _RES.get(name, None)
+        fn.restype = _RES.get(name, _RES.get(name + "_v2"))
+        if plain:
+            setattr(lib, plain, fn)                # the header's macro names, as C callers see them
     return lib
 
 

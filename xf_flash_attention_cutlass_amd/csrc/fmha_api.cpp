@@ -205,6 +205,9 @@ bool check_common(const void* q, const void* k, const void* v, const void* o, in
         return fail(1, "Number of heads in key/value must divide number of heads in query (h=%d, hk=%d)", h, hk);
     if (d <= 0 || d % 8 != 0) return fail(1, "head_size must be a positive multiple of 8 (got %d)", d);
     if (d > 256) return fail(1, "FlashAttention forward only supports head dimension at most 256 (got %d)", d);
+    // the kernels move 16-byte chunks (b128 buffer loads, LDS-DMA, 16-byte stores)
+    if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15)
+        return fail(1, "q/k/v/o must be 16-byte aligned device pointers");
     return true;
 }
 
@@ -222,8 +225,10 @@ void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
 thread_local uint64_t g_seed = 0, g_offset = 0;
 
 template <typename P>
-bool set_dropout(P& p, float p_dropout) {
+bool set_dropout(P& p, float p_dropout, float softcap) {
     if (!(p_dropout >= 0.f && p_dropout < 1.f)) return fail(1, "p_dropout must be in [0, 1) (got %g)", p_dropout);
+    // the reference's rule (export.cpp:515,737; flash_api_hip.cpp:400,606,895,1128)
+    if (softcap > 0.f && p_dropout > 0.f) return fail(1, "Softcapping does not support dropout for now");
     p.drop = p_dropout > 0.f;
     if (!p.drop) return true;
     const float keep = 1.f - p_dropout;                   // paged_attn.cpp:106-113
@@ -325,7 +330,7 @@ extern "C" {
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
-const char* fmha_version(void) { return "xf-fmha-gfx950 2.0"; }
+const char* fmha_version(void) { return "xf-fmha-gfx950 2.1"; }
 
 void fmha_set_rng_state(uint64_t seed, uint64_t offset) { g_seed = seed; g_offset = offset; }
 
@@ -399,7 +404,7 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes_ptr;
         p.alibi_bstride = batch_size > 1 ? num_heads : 0;   // paged_attn.cpp:375
-        if (!set_dropout(p, p_dropout)) return;
+        if (!set_dropout(p, p_dropout, softcap)) return;
         run_fwd(p, !is_fp16, stream, num_splits);
         if (return_softmax && g_status == 0) run_sdmask(p, p_ptr, !is_fp16, stream);
     } catch (...) {
@@ -419,6 +424,14 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
         REQUIRE(st != nullptr, "strides must be non-null");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
         for (int i = 0; i < 12; ++i) REQUIRE(st[i] >= 0, "strides must be non-negative");
+        {   // (a stride over an extent of 1 is never applied)
+            const int ext[12] = {batch_size, seqlen_q, num_heads, batch_size, seqlen_k, num_heads_k,
+                                 batch_size, seqlen_k, num_heads_k, batch_size, seqlen_q, num_heads};
+            for (int i = 0; i < 12; ++i)
+                REQUIRE(ext[i] == 1 || st[i] % 8 == 0,
+                        "strides must be multiples of 8 elements (16 bytes): stride %d is %lld", i,
+                        (long long)st[i]);
+        }
         // one sequence's slab of each tensor, addressed with 32-bit offsets by the kernels
         auto slab = [&](const char* what, int rows, int64_t row, int64_t head, int heads) {
             const int64_t bytes = ((int64_t)(rows - 1) * row + (int64_t)(heads - 1) * head + head_size) * 2;
@@ -445,7 +458,7 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
         p.alibi = (const float*)alibi_slopes;
         p.alibi_bstride = batch_size > 1 ? num_heads : 0;
         REQUIRE(!s_dmask || (p_dropout > 0.f && softmax_lse), "s_dmask needs p_dropout > 0 and softmax_lse");
-        if (!set_dropout(p, p_dropout)) return;
+        if (!set_dropout(p, p_dropout, softcap)) return;
         run_fwd(p, !is_fp16, stream, num_splits);
         if (s_dmask && g_status == 0) run_sdmask(p, s_dmask, !is_fp16, stream);
     } catch (...) {
@@ -545,7 +558,7 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
         REQUIRE(!s_dmask || (p_dropout > 0.f && softmax_lse && !block_table),
                 "s_dmask needs p_dropout > 0, softmax_lse and a non-paged K/V");
         REQUIRE(p_dropout == 0.f || !block_table, "dropout over a paged K/V cache is not supported");
-        if (!set_dropout(p, p_dropout)) return;
+        if (!set_dropout(p, p_dropout, softcap)) return;
         run_fwd(p, !is_fp16, stream, 1);
         if (s_dmask && g_status == 0) run_sdmask(p, s_dmask, !is_fp16, stream);
     } catch (...) {
@@ -684,14 +697,15 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
 
 
 // ------------------------------------------------------------------ backward -----------
-// Workspace: fp32 dq_accum [tokens][h][HD] (deterministic: one such slice per 256-key block of
-// the longest sequence, summed in key-block order by the convert kernel — NOT the reference's
-// split count ceil(CUs / (b*h)) of export.cpp:1090-1091, so it grows with seqlen_k; capped at
-// kMaxDetWorkspace with an error) + fp32 D = rowsum(dO*O) [tokens][h].
-constexpr size_t kMaxDetWorkspace = (size_t)32 << 30;
+// Workspace: fp32 dq_accum [tokens][h][HD] + fp32 D = rowsum(dO*O) [tokens][h].  Deterministic:
+// S = ceil(CUs / (b * hk)) dq_accum slices (the reference's bound, export.cpp:1090-1091, which
+// counts query heads: here a workgroup covers a kv head's whole GQA group), independent of
+// seqlen_k; workgroup (bh, s) adds key blocks s, s + S, ... into slice s in order.
 static int bwd_block_n_host(int d) { return hd_bucket(d) > 128 ? 128 : 256; }
-static int bwd_slices(int max_seqlen_k, int d, bool det) {
-    return det ? (max_seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d) : 1;
+static int bwd_slices(int batch, int hk, bool det) {
+    if (!det) return 1;
+    const int units = std::max(1, batch * hk);
+    return std::max(1, (num_cus(current_device()) + units - 1) / units);
 }
 static size_t bwd_acc_bytes(int64_t tokens, int h, int d) {
     return (((size_t)tokens * h * hd_bucket(d) * sizeof(float)) + 255) / 256 * 256;
@@ -701,18 +715,18 @@ static size_t bwd_ws_bytes(int64_t tokens, int h, int d, int slices) {
     return (size_t)slices * bwd_acc_bytes(tokens, h, d) + ((dsum + 255) / 256) * 256;
 }
 
-size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
-                               int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size,
+size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t /*seqlen_k*/, int32_t batch_size,
+                               int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                bool deterministic) {
     return bwd_ws_bytes((int64_t)batch_size * seqlen_q, num_heads, head_size,
-                        bwd_slices(seqlen_k, head_size, deterministic));
+                        bwd_slices(batch_size, num_heads_k, deterministic));
 }
 
-size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t /*batch_size*/,
-                                      int32_t num_heads, int32_t /*num_heads_k*/, int32_t head_size,
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t /*max_seqlen_k*/, int32_t batch_size,
+                                      int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                       bool deterministic) {
     return bwd_ws_bytes(total_q, num_heads, head_size,
-                        bwd_slices(max_seqlen_k, head_size, deterministic));
+                        bwd_slices(batch_size, num_heads_k, deterministic));
 }
 
 // The pre / convert kernels index (token, head, 16-byte chunk) with one 32-bit thread id.
@@ -749,18 +763,16 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
+        REQUIRE(!(softcap > 0.f && p_dropout > 0.f), "Softcapping does not support dropout for now");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive");
         const int h = num_heads, hk = num_heads_k, d = head_size;
         if (!slab_ok("q/out/dout/dq", seqlen_q, (int64_t)h * d, 2) ||
             !slab_ok("k/v/dk/dv", seqlen_k, (int64_t)hk * d, 2) ||
             !slab_ok("dq_accum", seqlen_q, hd_bucket(d), 4) ||
             !bwd_rows_ok((int64_t)batch_size * seqlen_q, h, d)) return;
-        const int slices = bwd_slices(seqlen_k, d, deterministic);
+        const int slices = bwd_slices(batch_size, hk, deterministic);
         const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d, slices);
-        REQUIRE(!deterministic || need <= kMaxDetWorkspace,
-                "deterministic backward needs %zu bytes of dQ slices (one per 256-key block of seqlen_k "
-                "%d); the limit is %zu: use deterministic=False for this shape", need, seqlen_k,
-                kMaxDetWorkspace);
+        const int nkb = (seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
@@ -772,7 +784,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes((int64_t)batch_size * seqlen_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
-        p.dq_slices = deterministic ? slices : 0;
+        p.dq_slices = deterministic ? std::min(slices, nkb) : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = (int64_t)seqlen_q * h * d;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = p.q_batch;
@@ -789,7 +801,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, seqlen_k);
-        if (!set_dropout(p, p_dropout)) return;
+        if (!set_dropout(p, p_dropout, softcap)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_bwd");
@@ -810,6 +822,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
+        REQUIRE(!(softcap > 0.f && p_dropout > 0.f), "Softcapping does not support dropout for now");
         REQUIRE(cu_seqlens_q && cu_seqlens_k, "cu_seqlens_q/cu_seqlens_k must be non-null");
         REQUIRE(total_q > 0 && total_k > 0 && max_seqlen_q > 0 && max_seqlen_k > 0,
                 "total/max sequence lengths must be positive");
@@ -818,12 +831,9 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
             !slab_ok("k/v/dk/dv", max_seqlen_k, (int64_t)hk * d, 2) ||
             !slab_ok("dq_accum", max_seqlen_q, hd_bucket(d), 4) ||
             !bwd_rows_ok(total_q, h, d)) return;
-        const int slices = bwd_slices(max_seqlen_k, d, deterministic);
+        const int slices = bwd_slices(batch_size, hk, deterministic);
         const size_t need = bwd_ws_bytes(total_q, h, d, slices);
-        REQUIRE(!deterministic || need <= kMaxDetWorkspace,
-                "deterministic backward needs %zu bytes of dQ slices (one per 256-key block of "
-                "max_seqlen_k %d); the limit is %zu: use deterministic=False for this shape", need,
-                max_seqlen_k, kMaxDetWorkspace);
+        const int nkb = (max_seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d);
         char* ws = (char*)workspace;
         if (!ws) ws = (char*)pool_get(stream, need);
         else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
@@ -835,7 +845,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes(total_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
-        p.dq_slices = deterministic ? slices : 0;
+        p.dq_slices = deterministic ? std::min(slices, nkb) : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = 0;
@@ -854,7 +864,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, max_seqlen_k);
-        if (!set_dropout(p, p_dropout)) return;
+        if (!set_dropout(p, p_dropout, softcap)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "varlen backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_varlen_bwd");

@@ -43,8 +43,10 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
     });
     const int nkb = (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>();
     BwdParams pp = p;
-    pp.order = p.order && (p.b * p.hk) % 8 == 0;
-    const dim3 grid = pp.order ? dim3(p.b * p.hk * nkb) : dim3(p.b * p.hk, nkb);
+    pp.order = !p.dq_slices && p.order && (p.b * p.hk) % 8 == 0;
+    // deterministic: one workgroup per (batch x kv head, dQ slice), walking its key blocks
+    const dim3 grid = p.dq_slices ? dim3(p.b * p.hk, p.dq_slices)
+                    : pp.order ? dim3(p.b * p.hk * nkb) : dim3(p.b * p.hk, nkb);
     hipLaunchKernelGGL(kern, grid, dim3(bwd_waves<HD>() * 64), smem, st, pp);
     e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -17,8 +17,10 @@
 //  * dS crosses LDS once (as dS^T, bf16) for dQ = dS K, computed with v_mfma_f32_16x16x32 by
 //    all waves and added to an fp32 dQ accumulator with global float atomics (256 keys per
 //    workgroup => 640 MFMA flops per atomic byte, cdna_hip_programming.md Appendix B), or, in
-//    deterministic mode (export.cpp:1086-1092 splits dq_accum the same way), stored into the
-//    key block's own accumulator slice and summed in key-block order by the convert kernel;
+//    deterministic mode, into one of S = ceil(CUs / (b * hk)) accumulator slices (the bound of
+//    export.cpp:1090-1091): workgroup (bh, s) walks key blocks s, s + S, s + 2S, ... in order,
+//    retiring each block's atomics before the next, and the convert kernel sums the slices in
+//    order - bitwise reproducible, workspace independent of seqlen_k;
 //  * P is recomputed from the forward LSE; D = rowsum(dO*O) comes from the preprocess kernel.
 #pragma once
 
@@ -41,13 +43,10 @@ template <int HD> constexpr size_t bwd_smem_bytes() {
     return (bwd_v_in_regs<HD>() ? 1 : 2) * (size_t)bwd_block_n<HD>() * HD * 2 + 2 * (size_t)32 * HD * 2 +
            (size_t)bwd_block_n<HD>() * 64;
 }
-// dQ partial sums -> the fp32 accumulator: float atomics into one [rows][HD] accumulator, or
-// (deterministic) plain stores into this key block's own slice, summed in key-block order by
-// the convert kernel
-template <bool DET>
+// dQ partial sums -> the fp32 accumulator (deterministic mode: this workgroup's slice, which no
+// other workgroup touches) by float atomics
 __device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
-    if constexpr (DET) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
-    else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
 }
 constexpr int kBwdBlockM = 32;               // query rows per tile
 
@@ -74,7 +73,7 @@ __device__ __forceinline__ int ds_off(int row, int col) {
 }
 
 // ---------------------------------------------------------------- preprocess ---------------
-// D[row] = sum_d dO*O (fp32), and zero the fp32 dQ accumulator row.
+// D[row] = sum_d dO*O (fp32), and zero the fp32 dQ accumulator row (of every slice).
 template <int HD, typename T>
 __global__ void __launch_bounds__(256) fmha_bwd_pre_kernel(const BwdParams p, int total_rows) {
     constexpr int TPR = HD / 8;                 // threads per (token, head) row
@@ -104,16 +103,17 @@ __global__ void __launch_bounds__(256) fmha_bwd_pre_kernel(const BwdParams p, in
     for (int m = TPR / 2; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
     const int64_t li = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + pos;
     if (c == 0) p.dsum[li] = acc;
-    if (p.dq_slices) return;    // deterministic: every slice row read by convert is stored first
     float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
                 (int64_t)pos * p.acc_row + d0;
-    *reinterpret_cast<f32x4_t*>(qa) = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    *reinterpret_cast<f32x4_t*>(qa + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int ns = p.dq_slices ? p.dq_slices : 1;
+    for (int s = 0; s < ns; ++s, qa += p.acc_slice) {
+        *reinterpret_cast<f32x4_t*>(qa) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4_t*>(qa + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
 }
 
-// dQ = dQaccum * scale -> dtype.  Deterministic mode: dQaccum = the sum, in key-block order, of
-// the slices of the key blocks whose query-tile sweep covered this row (the same [p_lo, p_hi)
-// tile range the main kernel computes; other slice rows are never written).
+// dQ = dQaccum * scale -> dtype.  Deterministic mode: dQaccum = the slices summed in slice
+// order (slice s holds key blocks s, s + S, ... added in that order by one workgroup).
 template <int HD, typename T>
 __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p, int total_rows) {
     constexpr int TPR = HD / 8;
@@ -132,38 +132,11 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
                       (int64_t)pos * p.acc_row + d0;
     float acc[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    if (!p.dq_slices) {
+    for (int j = 0; j < 8; ++j) acc[j] = qa[j];
+    for (int s = 1; s < p.dq_slices; ++s) {
+        qa += p.acc_slice;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = qa[j];
-    } else {
-        constexpr int BN = bwd_block_n<HD>();
-        int sq = p.seqlen_q, sk = p.seqlen_k, lpos = pos;
-        if (p.cu_seqlens_q) {     // varlen: the sequence holding global token `tok`
-            int lo = 0, hi = p.b - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (p.cu_seqlens_q[mid] <= tok) lo = mid; else hi = mid - 1;
-            }
-            lpos = tok - p.cu_seqlens_q[lo];
-            sq = p.cu_seqlens_q[lo + 1] - p.cu_seqlens_q[lo];
-            sk = p.cu_seqlens_k[lo + 1] - p.cu_seqlens_k[lo];
-        }
-        const bool mask = p.wl >= 0 || p.wr >= 0;
-        const int diag = sk - sq;
-        const int tile = lpos / kBwdBlockM;
-        for (int j = 0; j < p.dq_slices; ++j) {
-            const int n0 = j * BN;
-            if (n0 >= sk) break;
-            int p_lo = 0, p_hi = sq;
-            if (mask && p.wr >= 0) p_lo = max(0, n0 - diag - p.wr);
-            if (mask && p.wl >= 0) p_hi = min(sq, n0 + BN - 1 - diag + p.wl + 1);
-            if (p_hi <= p_lo) continue;
-            if (tile < p_lo / kBwdBlockM || tile >= (p_hi + kBwdBlockM - 1) / kBwdBlockM) continue;
-            const float* sl = qa + (int64_t)j * p.acc_slice;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u] += sl[u];
-        }
+        for (int j = 0; j < 8; ++j) acc[j] += qa[j];
     }
     typedef __attribute__((ext_vector_type(8))) T T8;
     T8 v;
@@ -175,10 +148,11 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
 }
 
 // ---------------------------------------------------------------- main ---------------------
-// DET (deterministic dQ slices) is instantiated only with MASK = FEAT = true, whose runtime
-// tests cover every window / feature combination.
-template <int HD, typename T, bool MASK, bool FEAT, bool DET = false>
-__global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
+// One key block kb (BN keys) of one (batch, kv head) bh: dK / dV of its keys, dQ partial sums
+// added into dq_base (the accumulator, or this workgroup's deterministic slice).
+template <int HD, typename T, bool MASK, bool FEAT>
+__device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, const int bh, const int kb,
+                                              float* const dq_base) {
     using V8 = typename DT<T>::v8;
     constexpr int NW = bwd_waves<HD>();
     constexpr int BN = bwd_block_n<HD>();
@@ -202,7 +176,6 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     constexpr int QLD = BQ * CPR / NT;          // Q (and dO) chunks per thread
     static_assert(QLD >= 1 && BQ * CPR == QLD * NT, "Q/dO tile geometry");
 
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     char* k_lds = smem;
     char* v_lds = smem + KT_BYTES;                   // (unused when VR)
     char* q_lds = smem + (VR ? 1 : 2) * KT_BYTES;
@@ -215,15 +188,6 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
     const int lr = lane & 31;
     const int hh = lane >> 5;
 
-    // order 1: workgroup w runs on XCD w % 8 (dispatch round-robin); XCD x takes the kv heads
-    // bh = x (mod 8), each with its key blocks consecutive, heaviest (causal) first
-    int bh = blockIdx.x, kb = blockIdx.y;
-    if (p.order) {
-        const int nkb = (p.seqlen_k + BN - 1) / BN;
-        const int i = (int)(blockIdx.x >> 3);
-        bh = (int)(blockIdx.x & 7) + 8 * (i / nkb);
-        kb = i - (i / nkb) * nkb;
-    }
     const int bidx = bh / p.hk;
     const int hk_i = bh - bidx * p.hk;
     const int n0 = kb * BN;
@@ -415,7 +379,6 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
         for (int dt = 0; dt < ND; ++dt) { dk[ks][dt] = f32x16{}; dv[ks][dt] = f32x16{}; }
 
     const float c = p.scale_log2;
-    float* const dq_base = p.dq_accum + (DET ? (int64_t)kb * p.acc_slice : 0);
     float lsd_cur = 0.f;
     float* const lsd_slot = reinterpret_cast<float*>(ds_lds + wave * kBwdKeysPerWave * 64);
     if (n_iter > 0) { load_q(0); }
@@ -621,7 +584,7 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                 const int base = d < p.d ? (16 * mt + 4 * g16) * arow + d * 4 : kOOB;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    dq_add<DET>(dq[i][r], qrs, base + r * arow);
+                    dq_add(dq[i][r], qrs, base + r * arow);
             }
         }
         __syncthreads();
@@ -651,6 +614,38 @@ __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmh
                     *reinterpret_cast<T4*>(dvr + d) = vv;
                 }
             }
+    }
+}
+
+// DET (deterministic dQ) is instantiated only with MASK = FEAT = true, whose runtime tests cover
+// every window / feature combination.
+template <int HD, typename T, bool MASK, bool FEAT, bool DET = false>
+__global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BN = bwd_block_n<HD>();
+    const int nkb = (p.seqlen_k + BN - 1) / BN;
+    if constexpr (DET) {
+        // workgroup (bh, s) owns dQ slice s and walks key blocks s, s + S, s + 2S, ... (S =
+        // gridDim.y slices) in order; each block's atomics are retired (vmcnt(0)) before the
+        // next block issues its own, so every dQ element receives its adds in key-block order
+        float* const slice = p.dq_accum + (int64_t)blockIdx.y * p.acc_slice;
+        for (int kb = (int)blockIdx.y; kb < nkb; kb += (int)gridDim.y) {
+            if (kb != (int)blockIdx.y) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+            bwd_key_block<HD, T, MASK, FEAT>(p, smem, (int)blockIdx.x, kb, slice);
+        }
+    } else {
+        // order 1: workgroup w runs on XCD w % 8 (dispatch round-robin); XCD x takes the kv
+        // heads bh = x (mod 8), each with its key blocks consecutive, heaviest (causal) first
+        int bh = blockIdx.x, kb = blockIdx.y;
+        if (p.order) {
+            const int i = (int)(blockIdx.x >> 3);
+            bh = (int)(blockIdx.x & 7) + 8 * (i / nkb);
+            kb = i - (i / nkb) * nkb;
+        }
+        bwd_key_block<HD, T, MASK, FEAT>(p, smem, bh, kb, p.dq_accum);
     }
 }
 

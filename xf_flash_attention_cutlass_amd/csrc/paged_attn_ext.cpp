@@ -42,6 +42,22 @@ at::Tensor pad_last(const at::Tensor& t, int d_og) {
     return torch::nn::functional::pad(t, torch::nn::functional::PadFuncOptions({0, 8 - d_og % 8}));
 }
 
+// The kernels move 16-byte chunks (b128 buffer loads, LDS-DMA, 16-byte row stores): every base
+// pointer must be 16-byte aligned and every row / head / batch stride a multiple of 16 bytes.
+bool aligned16(const at::Tensor& t) {
+    if ((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) != 0) return false;
+    for (int i = 0; i + 1 < t.dim(); ++i)
+        if (t.size(i) > 1 && (t.stride(i) * (int64_t)t.element_size()) % 16 != 0) return false;
+    return true;
+}
+
+// contiguous AND 16-byte aligned (a view at an odd storage offset is copied)
+at::Tensor dense(const at::Tensor& t) {
+    at::Tensor c = t.contiguous();
+    if (!aligned16(c)) c = c.clone(at::MemoryFormat::Contiguous);
+    return c;
+}
+
 void check_qkv_dtype(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
     auto dt = q.dtype();
     TORCH_CHECK(dt == torch::kFloat16 || dt == torch::kBFloat16,
@@ -119,6 +135,7 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     TORCH_CHECK(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
     if (window_size_left >= seqlen_k) window_size_left = -1;
     if (window_size_right >= seqlen_k) window_size_right = -1;
@@ -128,12 +145,13 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     CHECK_SHAPE(k, batch_size, seqlen_k, num_heads_k, head_size_og);
     CHECK_SHAPE(v, batch_size, seqlen_k, num_heads_k, head_size_og);
 
-    // d % 8 == 0: strided views (head / batch slices) run in place through fmha_fwd_strided;
-    // otherwise the reference's padding to a multiple of 8 (export.cpp:539-547)
-    const bool strided = head_size_og % 8 == 0;
-    at::Tensor q_padded = strided ? q : pad_last(q, head_size_og).contiguous();
-    at::Tensor k_padded = strided ? k : pad_last(k, head_size_og).contiguous();
-    at::Tensor v_padded = strided ? v : pad_last(v, head_size_og).contiguous();
+    // d % 8 == 0 and 16-byte aligned: strided views (head / batch slices, kvpacked kv[:, :, 0])
+    // run in place through fmha_fwd_strided; otherwise the reference's padding to a multiple of
+    // 8 (export.cpp:539-547) into aligned contiguous copies
+    const bool strided = head_size_og % 8 == 0 && aligned16(q) && aligned16(k) && aligned16(v);
+    at::Tensor q_padded = strided ? q : dense(pad_last(q, head_size_og));
+    at::Tensor k_padded = strided ? k : dense(pad_last(k, head_size_og));
+    at::Tensor v_padded = strided ? v : dense(pad_last(v, head_size_og));
     at::Tensor out;
     if (out_.has_value()) {
         out = out_.value();
@@ -141,7 +159,8 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
         CHECK_DEVICE(out);
         TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
         CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size_og);
-        if (head_size_og % 8 != 0) out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
+        if (head_size_og % 8 != 0 || !aligned16(out) || (!strided && !out.is_contiguous()))
+            out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
     } else {
         out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
     }
@@ -214,6 +233,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     TORCH_CHECK(head_size_og <= 256, "FlashAttention forward only supports head dimension at most 256");
     TORCH_CHECK(num_heads % num_heads_k == 0, "Number of heads in key/value must divide number of heads in query");
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     TORCH_CHECK(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
     TORCH_CHECK(p_dropout == 0.f || !paged_KV, "dropout over a paged K/V cache is not supported");
     const int max_num_blocks_per_seq = !paged_KV ? 0 : block_table.size(1);
@@ -243,9 +263,9 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
         TORCH_CHECK(seqused.is_contiguous(), "seqused_k must be contiguous");
         CHECK_SHAPE(seqused, batch_size);
     }
-    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
-    at::Tensor k_padded = pad_last(k, head_size_og).contiguous();
-    at::Tensor v_padded = pad_last(v, head_size_og).contiguous();
+    at::Tensor q_padded = dense(pad_last(q, head_size_og));
+    at::Tensor k_padded = dense(pad_last(k, head_size_og));
+    at::Tensor v_padded = dense(pad_last(v, head_size_og));
     at::Tensor out;
     if (out_.has_value()) {
         out = out_.value();
@@ -253,7 +273,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
         CHECK_DEVICE(out);
         TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
         CHECK_SHAPE(out, sizes[0], sizes[1], head_size_og);
-        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+        if (head_size_og % 8 != 0 || !out.is_contiguous() || !aligned16(out)) out = torch::empty_like(q_padded);
     } else {
         out = torch::empty_like(q_padded);
     }
@@ -356,9 +376,9 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
         CHECK_SHAPE(vcache, num_blocks, page_block_size, num_heads_k, head_size_og);
         CHECK_SHAPE(block_table, batch_size, max_num_blocks_per_seq);
     }
-    at::Tensor q_padded = pad_last(q, head_size_og).contiguous();
-    at::Tensor kc = pad_last(kcache, head_size_og).contiguous();
-    at::Tensor vc = pad_last(vcache, head_size_og).contiguous();
+    at::Tensor q_padded = dense(pad_last(q, head_size_og));
+    at::Tensor kc = dense(pad_last(kcache, head_size_og));
+    at::Tensor vc = dense(pad_last(vcache, head_size_og));
     at::Tensor out;
     if (out_.has_value()) {
         out = out_.value();
@@ -366,7 +386,7 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
         CHECK_DEVICE(out);
         TORCH_CHECK(out.stride(-1) == 1, "Output tensor must have contiguous last dimension");
         CHECK_SHAPE(out, batch_size, seqlen_q, num_heads, head_size_og);
-        if (head_size_og % 8 != 0 || !out.is_contiguous()) out = torch::empty_like(q_padded);
+        if (head_size_og % 8 != 0 || !out.is_contiguous() || !aligned16(out)) out = torch::empty_like(q_padded);
     } else {
         out = torch::empty_like(q_padded);
     }
@@ -471,7 +491,7 @@ static at::Tensor grad_out(c10::optional<at::Tensor>& t, const at::Tensor& like)
         TORCH_CHECK(x.dtype() == like.dtype(), "gradient must have the same dtype as its input");
         CHECK_DEVICE(x);
         TORCH_CHECK(x.sizes() == like.sizes(), "gradient has the wrong shape");
-        if (x.is_contiguous()) return x;
+        if (x.is_contiguous() && aligned16(x)) return x;
     }
     return torch::empty_like(like, like.options().memory_format(at::MemoryFormat::Contiguous));
 }
@@ -493,6 +513,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     TORCH_CHECK(dout.dtype() == q.dtype(), "query and dout must have the same dtype");
     CHECK_DEVICE(out); CHECK_DEVICE(dout); CHECK_DEVICE(softmax_lse);
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     dropout_rng_restore(p_dropout, rng_state);
     const auto sizes = q.sizes();
     const int batch_size = sizes[0];
@@ -516,13 +537,13 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     CHECK_SHAPE(dout, batch_size, seqlen_q, num_heads, head_size_og);
     CHECK_SHAPE(softmax_lse, batch_size, num_heads, seqlen_q);
     at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
-    at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
+    at::Tensor dout_padded = dense(pad_last(dout, head_size_og));
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
     auto softmax_d = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
-    auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
+    auto qc = dense(q), kc = dense(k), vc = dense(v), oc = dense(out);
     auto lse = softmax_lse.contiguous();
     const size_t ws = fmha_bwd_workspace_size(seqlen_q, seqlen_k, batch_size, num_heads, num_heads_k,
                                               head_size, deterministic);
@@ -562,6 +583,7 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     check_qkv_dtype(q, k, v);
     if (is_causal) window_size_right = 0;
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
+    if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     dropout_rng_restore(p_dropout, rng_state);
     TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
     TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
@@ -580,13 +602,13 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     CHECK_SHAPE(out, total_q, num_heads, head_size);
     CHECK_SHAPE(dout, total_q, num_heads, head_size_og);
     at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
-    at::Tensor dout_padded = pad_last(dout, head_size_og).contiguous();
+    at::Tensor dout_padded = dense(pad_last(dout, head_size_og));
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
     auto opts = q.options();
     auto softmax_d = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
-    auto qc = q.contiguous(), kc = k.contiguous(), vc = v.contiguous(), oc = out.contiguous();
+    auto qc = dense(q), kc = dense(k), vc = dense(v), oc = dense(out);
     auto lse = softmax_lse.contiguous();
     const size_t ws = fmha_varlen_bwd_workspace_size(total_q, max_seqlen_k, batch_size, num_heads,
                                                      num_heads_k, head_size, deterministic);
@@ -638,7 +660,7 @@ mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& v
     if (window_size_left >= seqlen_k) window_size_left = -1;
     if (window_size_right >= seqlen_k) window_size_right = -1;
     at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
-    auto qc = q.contiguous();
+    auto qc = dense(q);
     auto out = torch::empty_like(qc);
     auto lse = torch::empty({batch_size, num_heads, seqlen_q}, q.options().dtype(at::kFloat));
     auto bt = block_table.contiguous();
