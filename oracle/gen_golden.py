@@ -132,6 +132,42 @@ def case_fwd(ref, name, *, b, h, hk, sq, sk, d, dtype, causal, local=False, alib
     return t
 
 
+def case_dropout(ref, name, *, b, h, hk, sq, sk, d, dtype, causal, p_drop):
+    """attention_ref's dropout branch (test.py:387-394, used by test_flash_attn_output with
+    dropout_p > 0 and the kernel's S_dmask, test.py:873-935): a seeded keep mask stands in for
+    the kernel's, the reference's fp32 oracle output and gradients are stored; the restatement
+    is pinned against them bit for bit (both twins, outputs and gradients)."""
+    torch.random.manual_seed(0)
+    q = torch.randn(b, sq, h, d, dtype=dtype)
+    k = torch.randn(b, sk, hk, d, dtype=dtype)
+    v = torch.randn(b, sk, hk, d, dtype=dtype)
+    keep = torch.rand(b, h, sq, sk) >= p_drop
+    g = torch.randn(b, sq, h, d, dtype=dtype)
+    outs = {}
+    for up in (True, False):
+        qg, kg, vg = (x.clone().requires_grad_(True) for x in (q, k, v))
+        o, _ = ref["attention_ref"](qg, kg, vg, None, None, None, p_drop, keep, causal=causal,
+                                    upcast=up, reorder_ops=not up)
+        mq, mk, mv = (x.clone().requires_grad_(True) for x in (q, k, v))
+        mo, _ = ours.attention_ref(mq, mk, mv, None, None, None, p_drop, keep, causal=causal,
+                                   upcast=up, reorder_ops=not up)
+        tag = "ref" if up else "pt"
+        _same(mo.detach(), o.detach(), f"{name}:out_{tag}")
+        rg = _grads(o, (qg, kg, vg), g)
+        for n, a, r in zip(("dq", "dk", "dv"), _grads(mo, (mq, mk, mv), g), rg):
+            _same(a, r, f"{name}:{n}_{tag}")
+        outs[tag] = (o, *rg)
+    o_ref, dq, dk, dv = outs["ref"]
+    t = dict(q=q, k=k, v=v, dropout_mask=keep, dout=g, out_ref=o_ref, dq_ref=dq, dk_ref=dk,
+             dv_ref=dv)
+    meta = dict(kind="dropout", b=b, h=h, hk=hk, sq=sq, sk=sk, d=d,
+                dtype=str(dtype).split(".")[-1], causal=causal, window=[-1, -1], p_drop=p_drop,
+                softcap=0.0, alibi=False,
+                recipe="test.py:310-397 attention_ref dropout branch; seeded keep mask "
+                       "(torch.rand >= p), CPU, manual_seed(0)")
+    _save(name, t, meta, regen=("q", "k", "v", "dropout_mask", "dout"))
+
+
 def case_varlen(ref, name, *, b, h, hk, sq, sk, d, dtype, causal, local=False):
     """Recipe of test_flash_attn_varlen_output (test.py:1026-1307), CPU, seed 0."""
     torch.random.manual_seed(0)
@@ -270,6 +306,9 @@ def main():
     case_fwd(ref, "fwd_f16_b2h6hk2_q1k147_d128", b=2, h=6, hk=2, sq=1, sk=147, d=128,
              dtype=f16, causal=False, grads=False, save=save)
     if save:
+        # attention_ref's dropout branch (test.py:387-394)
+        case_dropout(ref, "dropout_f16_b2h4hk2_q97k131_d64_causal", b=2, h=4, hk=2, sq=97,
+                     sk=131, d=64, dtype=f16, causal=True, p_drop=0.17)
         # Varlen grid points (test.py:988-1025), downsized.
         case_varlen(ref, "varlen_f16_b4h3_q113k203_d64_causal", b=4, h=3, hk=3, sq=113, sk=203,
                     d=64, dtype=f16, causal=True)

@@ -48,6 +48,12 @@ def regenerate(m):
     t = {"q": torch.randn(b, sq, h, d, dtype=dt)}
     if m["kind"] == "kvcache":
         return t
+    if m["kind"] == "dropout":
+        t["k"] = torch.randn(b, sk, hk, d, dtype=dt)
+        t["v"] = torch.randn(b, sk, hk, d, dtype=dt)
+        t["dropout_mask"] = torch.rand(b, h, sq, sk) >= m["p_drop"]
+        t["dout"] = torch.randn(b, sq, h, d, dtype=dt)
+        return t
     if m.get("softcap", 0.0) > 0:
         t["q"] = t["q"] * m["softcap"]
     t["k"] = torch.randn(b, sk, hk, d, dtype=dt)

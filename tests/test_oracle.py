@@ -95,3 +95,18 @@ def test_parity_rule():
     assert ok and abs(bound - 0.012) < 1e-9
     ok, _, _ = orc.parity_ok(torch.full((4,), 0.02), ref, torch.full((4,), 0.006))
     assert not ok
+
+
+@pytest.mark.parametrize("name", gu.names("dropout"))
+def test_dropout_fixture_reproduced(name):
+    """attention_ref's dropout branch (test.py:387-394) against the reference's own outputs and
+    autograd gradients on a seeded keep mask (oracle/gen_golden.py case_dropout)."""
+    t, m = gu.load(name)
+    qq, kk, vv = (t[x].clone().requires_grad_(True) for x in ("q", "k", "v"))
+    out, _ = orc.attention_ref(qq, kk, vv, None, None, None, m["p_drop"], t["dropout_mask"],
+                               causal=m["causal"])
+    assert torch.equal(out, t["out_ref"]), name
+    grads = torch.autograd.grad(out, (qq, kk, vv), t["dout"])
+    for n, g in zip(("dq", "dk", "dv"), grads):
+        assert torch.equal(g, t[n + "_ref"]), f"{name}:{n}"
+    assert 0.75 < t["dropout_mask"].float().mean().item() < 0.91     # keep rate ~ 1 - p

@@ -64,6 +64,17 @@ def _worker(rank, world, port, kind, q):
             out, _ = sh.sharded_attention(x, k, v, local_fn=local, causal=True)
             ref = local(x, k, v, causal=True)
             ok = torch.allclose(out, ref, atol=1e-6)
+        elif kind == "heads_uneven":
+            # 3 kv heads over 2 ranks: query heads 4 / 2 gathered along dim 2 with padding
+            x = torch.randn(2, 30, 6, 16)
+            k = torch.randn(2, 30, 3, 16)
+            v = torch.randn(2, 30, 3, 16)
+
+            def local(qq, kk, vv, causal=False):
+                return orc.attention_ref(qq, kk, vv, causal=causal)[0]
+            out, qs = sh.sharded_attention(x, k, v, local_fn=local, causal=True)
+            ref = local(x, k, v, causal=True)
+            ok = torch.allclose(out, ref, atol=1e-6) and qs.size == (4 if rank == 0 else 2)
         elif kind == "heads_alibi":
             x = torch.randn(2, 24, 8, 16)
             k = torch.randn(2, 24, 4, 16)
@@ -133,7 +144,7 @@ def _worker(rank, world, port, kind, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["heads", "heads_alibi", "batch", "decode", "varlen"])
+@pytest.mark.parametrize("kind", ["heads", "heads_uneven", "heads_alibi", "batch", "decode", "varlen"])
 def test_sharded_world2_gloo(kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

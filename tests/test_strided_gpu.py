@@ -73,10 +73,12 @@ CASES = [  # b, s, h, hk, d  (the d128 bf16 cases are large enough for one pass 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("b,s,h,hk,d", CASES)
 def test_head_and_batch_sliced_views(xfa, dtype, causal, b, s, h, hk, d):
-    """q, k, v are head slices of wider tensors and batch slices of longer ones."""
+    """q, k, v are head slices of wider tensors and batch slices of longer ones (k and v with
+    the same row stride, as the 4-wave kernel's shared DMA offsets need: the same kernel runs as
+    for the contiguous copies, so the bytes must agree)."""
     qf = _randn((b + 2, s, h + 3, d), 1, dtype)
     kf = _randn((b + 2, s, hk + 2, d), 2, dtype)
-    vf = _randn((b + 2, s, hk + 1, d), 3, dtype)
+    vf = _randn((b + 2, s, hk + 2, d), 3, dtype)
     q = qf[1:b + 1, :, 2:h + 2].detach().requires_grad_(True)
     k = kf[2:b + 2, :, 1:hk + 1].detach().requires_grad_(True)
     v = vf[0:b, :, 1:hk + 1].detach().requires_grad_(True)
@@ -90,6 +92,20 @@ def test_head_and_batch_sliced_views(xfa, dtype, causal, b, s, h, hk, d):
     assert (dq.float() - dq_c.float()).abs().max().item() < 2e-2     # dQ atomics' order
     _oracle_check(f"sliced {b}x{s} h{h}/{hk} d{d} c{causal}", q, k, v, g, out, dq, dk, dv,
                   causal, ((0, 0), (b - 1, h - 1)))
+
+
+@pytest.mark.parametrize("b,s,h,hk,d", CASES)
+def test_sliced_views_k_v_row_strides_differ(xfa, b, s, h, hk, d):
+    """k and v slices of tensors with different head counts (k_row != v_row): the 8-wave
+    kernel's path; against the oracle."""
+    dtype = torch.bfloat16
+    q = _randn((b, s, h + 1, d), 21, dtype)[:, :, 1:].detach().requires_grad_(True)
+    k = _randn((b, s, hk + 3, d), 22, dtype)[:, :, :hk].detach().requires_grad_(True)
+    v = _randn((b, s, hk + 1, d), 23, dtype)[:, :, 1:].detach().requires_grad_(True)
+    g = _randn((b, s, h, d), 24, dtype)
+    out, dq, dk, dv = _run(xfa, q, k, v, g, True)
+    _oracle_check(f"k/v strides differ {b}x{s} h{h}/{hk} d{d}", q, k, v, g, out, dq, dk, dv,
+                  True, ((0, 0), (b - 1, h - 1)))
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

@@ -56,6 +56,10 @@ TILE = 64 * HD * 2    # bytes of one K (or V) tile
 VREG = 4 * TILE       # V ring after the K ring
 QK_LEAD = 6           # QK MFMAs before the first PV MFMA (the step's V^T reads land meanwhile)
 READ_LEAD = 5         # gaps between an LDS read and the MFMA that consumes it
+KS, VS = 4, 4         # K / V^T fragment ring slots (AGPRs a[192:192+4KS], a[256-4VS:256])
+NPRE, NVPRE = 2, 0    # K / V^T fragments of the next step read in this step's second half
+ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
+DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 
 # fixed registers (PS: the pre-scaled body, see set_mode; the map below is the legacy one)
 SBASE = (0, 64)       # S buffers A, B
@@ -126,7 +130,7 @@ def ktup(slot):
 
 
 def vtup(slot, half=None):
-    b = ABASE_V + 4 * slot
+    b = 256 - 4 * VS + 4 * slot
     if half is None:
         return f"a[{b}:{b + 3}]"
     return f"a[{b + 2 * half}:{b + 2 * half + 1}]"
@@ -181,7 +185,7 @@ def sm_value_ops(dt, v, src_buf, dst_buf, mask, nt):
     return ops
 
 
-def step_body(dt, ph, kind, mask, use_nm=True):
+def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
     """instructions of one step at ring phase ph (= j mod 4); use_nm: (PS) the QK^T chains
     start from C = -m (False only for tile 0, whose m is not known yet)"""
     par = ph & 1
@@ -190,8 +194,9 @@ def step_body(dt, ph, kind, mask, use_nm=True):
     kro = ((ph + 2) & 3) * TILE                          # K_{j+2}
     vro = (ph & 3) * TILE                                # V_j
     kno = ((ph + 3) & 3) * TILE                          # K_{j+3}: the next step's frags 0, 1
-    kdo = (ph & 3) * TILE                                # K_{j+4} (DMA)
-    vdo = VREG + ((ph + 2) & 3) * TILE                   # V_{j+2} (DMA)
+    kdo = ((ph + 1) if DMA2H else ph) % 4 * TILE       # K_{j+4} (DMA; DMA2H: K_{j+5})
+    vno = ((ph + 1) & 3) * TILE                          # V_{j+1}: the next step's first V^T frags
+    vdo = VREG + ((ph + 3) if DMA2H else (ph + 2)) % 4 * TILE   # V_{j+2} (DMA2H: V_{j+3})
 
     mf = mfma_order(kind)
     G = len(mf)
@@ -206,36 +211,50 @@ def step_body(dt, ph, kind, mask, use_nm=True):
             f = 2 * s + kt
             acc = sv(sn_buf, rb * 2 + kt)
             src = acc if s else (f"v[{NMB + 16 * rb}:{NMB + 16 * rb + 15}]" if PS and use_nm else "0")
-            mfma[g] = f"{mnem} {acc}, {ktup(f % 4)}, {qtup(rb, s)}, {src}"
+            mfma[g] = f"{mnem} {acc}, {ktup(f % KS)}, {qtup(rb, s)}, {src}"
             kfirst.setdefault(f, g); klast[f] = g
             need[g] = ("K", f)
         else:
             ks, d = a, b
             f = 4 * ks + d
             acc = otup(rb, d)
-            mfma[g] = f"{mnem} {acc}, {vtup(f % 4)}, {ptup(pc_buf, rb * 4 + ks)}, {acc}"
+            mfma[g] = f"{mnem} {acc}, {vtup(f % VS)}, {ptup(pc_buf, rb * 4 + ks)}, {acc}"
             vfirst.setdefault(f, g); vlast[f] = g
             need[g] = ("V", f)
 
     reads = []   # (gap, order, text, tag)
     if kind & QK:
-        for f in range(2, 16):
+        for f in range(NPRE, 16):
             s, kt = f // 2, f % 2
-            lo = klast[f - 4] + 2 if f >= 4 else 0
+            lo = klast[f - KS] + 2 if f >= KS else 0
             g = min(max(lo, kfirst[f] - READ_LEAD, 0), kfirst[f] - 1)
-            reads.append((g, 0, f"ds_read_b128 {ktup(f % 4)}, %[kb{s & 1}] offset:{kro + kt * 4 * RB + 512 * (s >> 1)}", ("K", f)))
+            reads.append((g, 0, f"ds_read_b128 {ktup(f % KS)}, %[kb{s & 1}] offset:{kro + kt * 4 * RB + 512 * (s >> 1)}", ("K", f)))
     if kind & PV:
-        for f in range(16):
+        for f in range(NVPRE, 16):
             ks, d = f // 4, f % 4
-            lo = vlast[f - 4] + 2 if f >= 4 else 0
+            lo = vlast[f - VS] + 2 if f >= VS else 0
             g = min(max(lo, vfirst[f] - READ_LEAD, 0), vfirst[f] - 1)
             off = vro + 2 * ks * RB + 512 * d
-            reads.append((g, 1, f"ds_read_b64_tr_b16 {vtup(f % 4, 0)}, %[vb0] offset:{off}", ("V", f)))
-            reads.append((g, 2, f"ds_read_b64_tr_b16 {vtup(f % 4, 1)}, %[vb1] offset:{off}", ("V", f)))
-    for f in (0, 1):
-        lo = max(mid + 1, (klast[12 + f] + 2) if (kind & QK) else 0)
-        g = max(lo, G - 8 + 2 * f)
-        reads.append((min(g, G), 3, f"ds_read_b128 {ktup(f)}, %[kb0] offset:{kno + f * 4 * RB}", ("N", f)))
+            reads.append((g, 1, f"ds_read_b64_tr_b16 {vtup(f % VS, 0)}, %[vb0] offset:{off}", ("V", f)))
+            reads.append((g, 2, f"ds_read_b64_tr_b16 {vtup(f % VS, 1)}, %[vb1] offset:{off}", ("V", f)))
+    # the next step's first K (K_{j+3}) and V^T (V_{j+1}) fragments, both published at this
+    # step's mid-point barrier, in one fixed order (the next step counts its waits on it)
+    gprev = mid + 1
+    for n, (w, f) in enumerate(prefetch_order()):
+        if w == "N":
+            lo = max(mid + 1, (klast[16 - KS + f] + 2) if (kind & QK) else 0)
+            g = max(lo, G - 8 + 2 * f, gprev)
+            s_, kt_ = f // 2, f % 2
+            txt = [f"ds_read_b128 {ktup(f)}, %[kb{s_ & 1}] offset:{kno + kt_ * 4 * RB + 512 * (s_ >> 1)}"]
+        else:
+            lo = max(mid + 1, (vlast[16 - VS + f] + 2) if (kind & PV) else 0)
+            g = max(lo, G - 8 + 2 * f, gprev)
+            off = vno + 2 * (f // 4) * RB + 512 * (f % 4)
+            txt = [f"ds_read_b64_tr_b16 {vtup(f, 0)}, %[vb0] offset:{off}",
+                   f"ds_read_b64_tr_b16 {vtup(f, 1)}, %[vb1] offset:{off}"]
+        gprev = g = min(g, G)
+        for i, t in enumerate(txt):
+            reads.append((g, 3 + 2 * n + i, t, (w, f)))
 
     def dma(which, i):
         # LDS-DMA piece i: 8 rows x 8 chunks; M0 = its LDS address (lane l lands at +16 l)
@@ -244,10 +263,10 @@ def step_body(dt, ph, kind, mask, use_nm=True):
         return [f"s_add_u32 m0, %[kdst], {base + i * 1024}",
                 f"buffer_load_dwordx4 %[dma{i}], {srd}, 0 offen lds"]
 
-    dmas = [(w, i) for i in range(4) for w in ("K", "V")]
+    dmas = [] if "nodma" in ABL else [(w, i) for i in range(4) for w in ("K", "V")]
     nt = 4 if (G in (0, 64) or PS) else 8
     sm = []      # (gap, seq, texts)
-    if kind & SM:
+    if kind & SM and not ("nosm" in ABL and kind & PV):
         span = G if G else 64
         for v in range(64):
             tg = (v * span) // 64
@@ -256,10 +275,13 @@ def step_body(dt, ph, kind, mask, use_nm=True):
 
     out = []
     if G == 0:
+        if DMA2H:
+            out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
         for w, i in dmas:
             a, b = dma(w, i)
             out += [a, "s_nop 0", b]
-        out += ["s_waitcnt vmcnt(8)", "s_barrier"]
+        if not DMA2H:
+            out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
         for _, _, txt in sorted(sm, key=lambda x: (x[0], x[1])):
             out += txt
         out += [r[2] for r in sorted(reads, key=lambda x: (x[0], x[1]))]
@@ -267,10 +289,17 @@ def step_body(dt, ph, kind, mask, use_nm=True):
 
     dma_gap = {}
     for n, wi in enumerate(dmas):
-        g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
+        if DMA2H:
+            g = min(mid + 1 + (n * max(1, G - mid - 4)) // len(dmas), G - 1)
+        else:
+            g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
-    issued = ["N0", "N1"]               # the previous step's prefetch of K frags 0, 1
-    last_idx = {("K", 0): 0, ("K", 1): 1}
+    # the previous step's prefetch of this step's first K / V^T fragments, in issue order
+    issued, last_idx = [], {}
+    for w, f in prefetch_order():
+        for _ in range(1 if w == "N" else 2):
+            issued.append((w, f))
+        last_idx[("K" if w == "N" else "V", f)] = len(issued) - 1
     waited = 0
     rby = {}
     for g, o, txt, tag in reads:
@@ -296,11 +325,14 @@ def step_body(dt, ph, kind, mask, use_nm=True):
             nd = need[g]
             if nd in last_idx and last_idx[nd] >= waited:
                 n = min(len(issued) - last_idx[nd] - 1, 15)
-                body.append(f"s_waitcnt lgkmcnt({n})")
+                if "nolgkm" not in ABL or not (kind & PV):
+                    body.append(f"s_waitcnt lgkmcnt({n})")
                 waited = len(issued) - n
             body.append(mfma[g])
             if g == mid:
-                body += ["s_waitcnt vmcnt(8)", "s_barrier"]
+                main = kind & PV
+                body += [] if ("novm" in ABL and main) else [f"s_waitcnt vmcnt({vm})"]
+                body += [] if ("nobar" in ABL and main) else ["s_barrier"]
         else:
             # past the last MFMA nothing separates a gap's v_exp from the next gap's use of its
             # result: a VALU reading a transcendental's result needs one wait state
@@ -317,11 +349,19 @@ def step_body(dt, ph, kind, mask, use_nm=True):
     return out
 
 
+def prefetch_order():
+    """the next step's fragments read at the end of a step: K frags 0..NPRE-1 ("N"), then V^T
+    frags 0..NVPRE-1 ("W")"""
+    return [("N", f) for f in range(NPRE)] + [("W", f) for f in range(NVPRE)]
+
+
 def step_prep():
-    """per step: the buffer descriptors of K_{j+4} and V_{j+2} (V clamped at tile 0): base
-    advanced to the tile, range = what is left of the workgroup's keys (>= 0)"""
-    out = [f"s_add_i32 s{ST}, s{SJ}, 4", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
-           f"s_add_i32 s{ST}, s{SJ}, 2", f"s_max_i32 s{ST}, s{ST}, 0",
+    """per step: the buffer descriptors of K_{j+4} and V_{j+2} (DMA2H: K_{j+5}, V_{j+3}; V
+    clamped at tile 0): base advanced to the tile, range = what is left of the workgroup's keys
+    (>= 0)"""
+    kl, vl = (5, 3) if DMA2H else (4, 2)
+    out = [f"s_add_i32 s{ST}, s{SJ}, {kl}", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
+           f"s_add_i32 s{ST}, s{SJ}, {vl}", f"s_max_i32 s{ST}, s{ST}, 0",
            f"s_mul_i32 s{SVO}, s{ST}, %[kstep]"]
     for r, lo, hi, off in ((SKR, "kblo", "kbhi", SKO), (SVR, "vblo", "vbhi", SVO)):
         out += [f"s_add_u32 s{r}, %[{lo}], s{off}", f"s_addc_u32 s{r + 1}, %[{hi}], 0",
@@ -432,6 +472,8 @@ def redo_block_ps(dt, par, uid):
 
 def redo_check(par, uid, tag):
     """after a step with SM: any lane's tile sum past the threshold -> rare path; l += tile sums"""
+    if "noredo" in ABL:
+        return [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
     return [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
             f"v_cmp_lt_f32_e64 s[{SCM}:{SCM + 1}], %[thr], v{LT + 1}",
             f"s_or_b64 vcc, vcc, s[{SCM}:{SCM + 1}]",
@@ -445,6 +487,29 @@ def redo_check(par, uid, tag):
             f".Lnr{tag}_{uid}:",
             f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}",
             f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
+
+
+def prologue_dma(dt):
+    """the DMA-only prologue steps, after the Q loads: K_0 published at step -3's barrier (and
+    Q landed), K_1 / V_0 in flight for the next steps"""
+    if not DMA2H:
+        out = [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
+        out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
+        return out + ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
+    # K_0 -> slot 0, K_1 -> slot 1 through both descriptor sets; then step -3 waits for all
+    # but K_1 (vmcnt 4: Q and K_0), publishes K_0 and issues K_2, V_0 after its barrier
+    out = []
+    for r, t in ((SKR, 0), (SVR, 1)):
+        off = "0" if t == 0 else "%[kstep]"
+        out += [f"s_add_u32 s{r}, %[kblo], {off}", f"s_addc_u32 s{r + 1}, %[kbhi], 0",
+                f"s_sub_i32 s{r + 2}, %[kvbytes], {off}", f"s_max_i32 s{r + 2}, s{r + 2}, 0",
+                f"s_mov_b32 s{r + 3}, 0x20000"]
+    for r, t in ((SKR, 0), (SVR, 1)):
+        for i in range(4):
+            out += [f"s_add_u32 m0, %[kdst], {t * TILE + i * 1024}", "s_nop 0",
+                    f"buffer_load_dwordx4 %[dma{i}], s[{r}:{r + 3}], 0 offen lds"]
+    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False, vm=4)
+    return out
 
 
 def item_program(dt, uid="%="):
@@ -462,9 +527,7 @@ def item_program(dt, uid="%="):
     for i in range(128):
         out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
     # prologue steps j = -4, -3: DMA only (K_0, K_1); j = -2: QK(0); rowmax; j = -1: QK(1)+SM(0)
-    out += [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
-    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
-    out += ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
+    out += prologue_dma(dt)
     out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(dt, 2, QK, False)
     # reference max of tile 0 (S in buffer A), masked in place
     out += ["s_nop 7", "s_nop 7", "s_nop 3"]
@@ -676,7 +739,9 @@ def ops():
     return [o.replace('"v"', '"a"') if o.split("]")[0][1:] in av else o for o in OPS]
 
 
-def emit():
+def emit(out=OUT):
+    assert 192 + 4 * KS <= 256 - 4 * VS and 16 % KS == 0 and 16 % VS == 0
+    assert NPRE <= KS and NVPRE <= VS and not (PS and (KS > 4 or VS > 4))
     lines = [
         "// GENERATED by tools/gen_fwd4.py -- do not edit by hand.",
         "// The 4-wave D = 128 forward's item body (fmha_fwd4_kernel.h): one asm statement with a",
@@ -701,10 +766,24 @@ def emit():
         lines.append("")
         print(dt, len(prog), "instructions/labels")
     lines.append("}  // namespace xfa")
-    open(OUT, "w").write("\n".join(lines) + "\n")
+    open(out, "w").write("\n".join(lines) + "\n")
 
 
 if __name__ == "__main__":
-    import sys
-    set_mode("--ps" in sys.argv)
-    emit()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ps", action="store_true", help="pre-scaled Q (not the default, DESIGN 3.1b)")
+    ap.add_argument("--ks", type=int, default=KS, help="K fragment ring slots")
+    ap.add_argument("--vs", type=int, default=VS, help="V^T fragment ring slots")
+    ap.add_argument("--lead", type=int, default=READ_LEAD, help="gaps an LDS read leads its MFMA")
+    ap.add_argument("--npre", type=int, default=NPRE, help="next-step K frags read early")
+    ap.add_argument("--nvpre", type=int, default=NVPRE, help="next-step V^T frags read early")
+    ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
+    ap.add_argument("--dma2h", action="store_true", help="DMA after the barrier, half a step more lead")
+    ap.add_argument("--out", default=OUT)
+    a = ap.parse_args()
+    set_mode(a.ps)
+    KS, VS, READ_LEAD, NPRE, NVPRE = a.ks, a.vs, a.lead, a.npre, a.nvpre
+    ABL = set(x for x in a.abl.split(",") if x)
+    DMA2H = a.dma2h
+    emit(a.out)

@@ -149,15 +149,6 @@ static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
 }
 #endif
 
-#if XFA_HD == 128 && defined(XFA_FWD4_STAMP)
-// diagnostics build: read and reset the 4-wave kernel's cycle stamps
-extern "C" void XFA_CAT(fmha_fwd4_stamp_, XFA_DTN)(unsigned long long* out) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd4_stamp), 4 * sizeof(unsigned long long));
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_stamp), z, sizeof(z));
-}
-#endif
-
 #if XFA_HD == 128
 // return_softmax with dropout (fmha_sdmask_kernel.h): s [b, h, sq_r, sk_r] in the q dtype
 hipError_t XFA_CAT(launch_sdmask_, XFA_DTN)(const FwdParams& p, void* s, int sq_r, int sk_r, hipStream_t st) {

@@ -21,7 +21,11 @@
 #pragma once
 
 #include "fmha_common.h"
+#ifdef XFA_FWD4_BODY
+#include XFA_FWD4_BODY          // an A/B variant of the generated body (tools/fwd4_variants.sh)
+#else
 #include "fmha_fwd4_body.h"
+#endif
 
 namespace xfa {
 
@@ -80,7 +84,6 @@ __device__ __forceinline__ void fwd4_item(const FwdParams& p, char* smem, const 
         t_w = lr_hi > 0 ? min(ntl, (lr_hi + kBlockN - 1) / kBlockN) - 1 : -1;
         e_w = lr_lo > 0 ? lr_lo / kBlockN : 0;
     }
-    if (p.fwd4 == 2) e_w = 0;                // debug: every tile through the masked body
     t_w = __builtin_amdgcn_readfirstlane(t_w);
     e_w = __builtin_amdgcn_readfirstlane(e_w);
 
@@ -165,7 +168,7 @@ __device__ __forceinline__ void fwd4_item(const FwdParams& p, char* smem, const 
     const int kstep = __builtin_amdgcn_readfirstlane(kBlockN * k_row * 2);
     (void)kvbytes;
     const int kdst = __builtin_amdgcn_readfirstlane(sbase + wave * 4096);
-    const float thr = p.fwd4 == 3 ? INFINITY : __builtin_amdgcn_exp2f(p.max_slack);   // 3: debug, no redo
+    const float thr = __builtin_amdgcn_exp2f(p.max_slack);
     if constexpr (BF16)
         fwd4_item_bf16(kblo, kbhi, vblo, vbhi, (int)kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma[0], dma[0] + 128, dma[1],
@@ -178,17 +181,10 @@ __device__ __forceinline__ void fwd4_item(const FwdParams& p, char* smem, const 
 
 // Persistent grid (one workgroup per CU) walking (b x kv head, row block) items in the
 // 8-wave kernel's orders: XCD-grouped pairs (dense) or per-XCD dynamic queues (varlen).
-#ifdef XFA_FWD4_STAMP
-static __device__ unsigned long long g_fwd4_stamp[4];
-#endif
 template <bool BF16>
 __global__ void __launch_bounds__(256, 1) fmha_fwd4_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_claim[2];
-#ifdef XFA_FWD4_STAMP
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long t_in = 0;
-#endif
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
     for (int k = 0;; ++k) {
@@ -227,21 +223,8 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd4_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
-#ifdef XFA_FWD4_STAMP
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         fwd4_item<BF16>(p, smem, bh, m_block);
-        t_in += __builtin_amdgcn_s_memtime() - t1;
-#else
-        fwd4_item<BF16>(p, smem, bh, m_block);
-#endif
     }
-#ifdef XFA_FWD4_STAMP
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&g_fwd4_stamp[0], t_in);
-        atomicAdd(&g_fwd4_stamp[1], __builtin_amdgcn_s_memtime() - t_start);
-        atomicAdd(&g_fwd4_stamp[2], 1ull);
-    }
-#endif
     if (p.persistent == 3 && threadIdx.x == 0) {
         const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
         if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {

@@ -90,22 +90,33 @@ def _slice_alibi(alibi, heads: Shard | None = None, batch: Shard | None = None):
 
 
 def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
-    """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank:
-    one all_gather_into_tensor of pieces padded to the largest, then a narrow per rank."""
+    """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank.
+
+    Even shards (the usual case: heads or batch divisible by the world size) take one
+    all_gather_into_tensor into a rank-major [world, *local.shape] buffer: for dim 0 that buffer
+    IS the result (no copy), otherwise one strided copy interleaves the ranks' pieces along
+    `dim`.  Uneven shards pad to the largest piece along `dim` and drop the padding afterwards."""
     dist, rank, world = _world()
     if world == 1:
         return local
+    local = local.contiguous()
     nmax = max(sizes)
+    if min(sizes) == nmax:
+        shape = list(local.shape)
+        gathered = local.new_empty([world * shape[0]] + shape[1:])      # rank-major along dim 0
+        dist.all_gather_into_tensor(gathered, local)
+        if dim == 0:
+            return gathered
+        shape[dim] = world * nmax
+        return gathered.view([world] + list(local.shape)).movedim(0, dim).reshape(shape)
     shape = list(local.shape)
     shape[dim] = nmax
     buf = local.new_zeros(shape)
     buf.narrow(dim, 0, local.shape[dim]).copy_(local)
-    buf = buf.movedim(dim, 0).contiguous()
-    gathered = local.new_empty([world * nmax] + list(buf.shape[1:]))   # rank-major
+    gathered = local.new_empty([world * shape[0]] + shape[1:])
     dist.all_gather_into_tensor(gathered, buf)
-    gathered = gathered.view([world, nmax] + list(buf.shape[1:]))
-    pieces = [gathered[r, :sizes[r]] for r in range(world)]
-    return torch.cat(pieces, dim=0).movedim(0, dim)
+    gathered = gathered.view([world] + shape)
+    return torch.cat([gathered[r].narrow(dim, 0, sizes[r]) for r in range(world)], dim=dim)
 
 
 def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
