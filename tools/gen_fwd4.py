@@ -29,7 +29,7 @@ reference (softmax_hip.h:129-189) up to rounding.
 Register map (per lane):
   a[0:127]    O^T accumulators, O[rb][dt] = a[64rb + 16dt : +15]
   a[128:191]  Q fragments (B operand of S^T), Q[rb][s] = a[128 + 32rb + 4s : +3]
-  a[192:207]  K fragment ring, frag f in slot f % 4 (frags 0, 1 of the next step read early)
+  a[192:223]  K fragment ring, frag f in slot f % 8 (frags 0..3 of the next step read early)
   a[240:255]  V^T fragment ring (4 slots)
   v[0:63]     S buffer A (4 accumulators rb*2 + kt);  v[64:127] S buffer B
   v[128:159]  P buffer A (8 x 4 dwords, rb*4 + ks);   v[160:191] P buffer B
@@ -55,9 +55,12 @@ RB = HD * 16          # bytes of one 8-row block of the kv_off image
 TILE = 64 * HD * 2    # bytes of one K (or V) tile
 VREG = 4 * TILE       # V ring after the K ring
 QK_LEAD = 6           # QK MFMAs before the first PV MFMA (the step's V^T reads land meanwhile)
-READ_LEAD = 5         # gaps between an LDS read and the MFMA that consumes it
-KS, VS = 4, 4         # K / V^T fragment ring slots (AGPRs a[192:192+4KS], a[256-4VS:256])
-NPRE, NVPRE = 2, 0    # K / V^T fragments of the next step read in this step's second half
+READ_LEAD = 8         # gaps between an LDS read and the MFMA that consumes it
+KS, VS = 8, 4         # K / V^T fragment ring slots (AGPRs a[192:192+4KS], a[256-4VS:256])
+NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's second half
+# (round 4, same-box A/B: the 8-slot K ring read 8 gaps ahead with 4 fragments prefetched
+#  across the step boundary +2..4 % over 4 slots / 5 gaps / 2; deeper V^T reads and the DMA
+#  issued after the barrier (DMA2H) did not add to it)
 ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 
@@ -355,10 +358,17 @@ def prefetch_order():
     return [("N", f) for f in range(NPRE)] + [("W", f) for f in range(NVPRE)]
 
 
-def step_prep():
+def step_prep(incr=False):
     """per step: the buffer descriptors of K_{j+4} and V_{j+2} (DMA2H: K_{j+5}, V_{j+3}; V
     clamped at tile 0): base advanced to the tile, range = what is left of the workgroup's keys
-    (>= 0)"""
+    (>= 0).  incr (the main loop, where the previous step's descriptors are one tile behind):
+    advance both by one tile, 8 SALU instead of 15"""
+    if incr:
+        out = []
+        for r in (SKR, SVR):
+            out += [f"s_add_u32 s{r}, s{r}, %[kstep]", f"s_addc_u32 s{r + 1}, s{r + 1}, 0",
+                    f"s_sub_i32 s{r + 2}, s{r + 2}, %[kstep]", f"s_max_i32 s{r + 2}, s{r + 2}, 0"]
+        return out
     kl, vl = (5, 3) if DMA2H else (4, 2)
     out = [f"s_add_i32 s{ST}, s{SJ}, {kl}", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
            f"s_add_i32 s{ST}, s{SJ}, {vl}", f"s_max_i32 s{ST}, s{ST}, 0",
@@ -561,7 +571,7 @@ def main_loop(dt, uid):
     for ph in range(4):
         par = ph & 1
         out.append(f".Lph{ph}_{uid}:")
-        out += step_prep() + lim_dec()
+        out += step_prep(incr=True) + lim_dec()
         out += [f"s_cmp_gt_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Li{ph}_{uid}",
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]

@@ -349,6 +349,7 @@ int fmha_set_option(const char* name, int value) {
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 1},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
         {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
+        {"fp8_w4", &o.fp8_w4, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -372,7 +373,7 @@ int fmha_get_option(const char* name) {
     XFA_GET(fwd_waves) XFA_GET(fwd_prio) XFA_GET(fwd_persistent) XFA_GET(fwd_slack)
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
     XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
-    XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold) XFA_GET(dec_bal)
+    XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold) XFA_GET(dec_bal) XFA_GET(fp8_w4)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;
@@ -498,6 +499,7 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
         p.order = op.fwd_order.load();
         p.max_slack = (float)op.fwd_slack.load();
         p.num_splits = 1;
+        p.fwd4 = op.fp8_w4.load();
         g_last_splits = 1;
         hip_ok(launch_fwd_fp8(p, out_fp16, stream), "fp8 forward launch");
     } catch (...) {

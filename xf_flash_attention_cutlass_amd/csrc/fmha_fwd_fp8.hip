@@ -1,9 +1,30 @@
 // fmha_fwd_fp8.hip — launches of the fp8 (e4m3fn) Q/K/V forward (fmha_fwd_fp8_kernel.h), D = 128,
 // bf16 or fp16 output; persistent XCD-paired grid as the bf16 forward.
 #include "fmha_fwd_fp8_kernel.h"
+#include "fmha_fwd8w_kernel.h"
 #include "fmha_launch.h"
 
 namespace xfa {
+
+// 4-wave fp8 forward (fmha_fwd8w_kernel.h): no left window (the 8-wave kernel's masked loop
+// handles those)
+template <bool F16>
+static hipError_t launch_fp8_w4(const FwdParams& p, hipStream_t st) {
+    const int n_mb = (p.seqlen_q * p.group + kFwd8wRows - 1) / kFwd8wRows;
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    dim3 grid(p.b * p.hk, n_mb, 1);
+    const int items = p.b * p.hk * n_mb;
+    if (p.persist_per_cu > 0 && items > p.num_cus) {
+        pp.persistent = (p.order == 1 && p.num_cus % 8 == 0) ? 2 : 1;
+        grid = dim3(p.num_cus, 1, 1);
+    }
+    static std::atomic<unsigned long long> attr_done{0};
+    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8w_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8wSmem); });
+    hipLaunchKernelGGL((fmha_fwd8w_kernel<F16>), grid, dim3(256), kFwd8wSmem, st, pp);
+    return hipGetLastError();
+}
 
 template <typename T>
 static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
@@ -35,6 +56,8 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
 }
 
 hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st) {
+    if (p.fwd4 && p.k_row == p.v_row && (p.wl < 0 || p.wl >= p.seqlen_k))
+        return out_fp16 ? launch_fp8_w4<true>(p, st) : launch_fp8_w4<false>(p, st);
     return out_fp16 ? launch_fp8_t<_Float16>(p, st) : launch_fp8_t<__bf16>(p, st);
 }
 
