@@ -63,6 +63,7 @@ NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's s
 #  issued after the barrier (DMA2H) did not add to it)
 ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
+WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
 
 # fixed registers (PS: the pre-scaled body, see set_mode; the map below is the legacy one)
 SBASE = (0, 64)       # S buffers A, B
@@ -522,6 +523,33 @@ def prologue_dma(dt):
     return out
 
 
+def next_k_reads(ph):
+    """the prefetch reads of the first NPRE K fragments of K_{j+3} at phase ph, in prefetch
+    order (what a DMA-only step at phase ph ends with)"""
+    kno = ((ph + 3) & 3) * TILE
+    out = []
+    for f in range(NPRE):
+        s_, kt_ = f // 2, f % 2
+        out.append(f"ds_read_b128 {ktup(f)}, %[kb{s_ & 1}] offset:{kno + kt_ * 4 * RB + 512 * (s_ >> 1)}")
+    return out
+
+
+def warm_issue(uid):
+    """item tail (all waves past their last LDS read): the next item's K_0 -> slot 0, K_1 ->
+    slot 1 by LDS-DMA, so its prologue does not wait for the first tiles' memory latency"""
+    out = [f"s_cmp_eq_u32 %[nxt], 0", f"s_cbranch_scc1 .Lnw_{uid}",
+           f"s_mov_b32 s{SKR}, %[kblo2]", f"s_mov_b32 s{SKR + 1}, %[kbhi2]",
+           f"s_mov_b32 s{SKR + 2}, %[kvb2]", f"s_mov_b32 s{SKR + 3}, 0x20000",
+           f"s_add_u32 s{SVR}, %[kblo2], %[kstep]", f"s_addc_u32 s{SVR + 1}, %[kbhi2], 0",
+           f"s_sub_i32 s{SVR + 2}, %[kvb2], %[kstep]", f"s_max_i32 s{SVR + 2}, s{SVR + 2}, 0",
+           f"s_mov_b32 s{SVR + 3}, 0x20000"]
+    for r, t in ((SKR, 0), (SVR, 1)):
+        for i in range(4):
+            out += [f"s_add_u32 m0, %[kdst], {t * TILE + i * 1024}", "s_nop 0",
+                    f"buffer_load_dwordx4 %[dma{i}], s[{r}:{r + 3}], 0 offen lds"]
+    return out + [f".Lnw_{uid}:"]
+
+
 def item_program(dt, uid="%="):
     out = ["s_waitcnt lgkmcnt(0)"]
     # constants, state
@@ -537,7 +565,14 @@ def item_program(dt, uid="%="):
     for i in range(128):
         out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
     # prologue steps j = -4, -3: DMA only (K_0, K_1); j = -2: QK(0); rowmax; j = -1: QK(1)+SM(0)
-    out += prologue_dma(dt)
+    if WARM:
+        # warm item: K_0 / K_1 were issued by the previous item's tail; Q, K_0 and K_1 landed
+        # (vmcnt(0)) and published (barrier), then step -3's reads of K_0
+        out += [f"s_cmp_eq_u32 %[warm], 0", f"s_cbranch_scc1 .Lcold_{uid}",
+                "s_waitcnt vmcnt(0)", "s_barrier"] + next_k_reads(1)
+        out += [f"s_branch .Lwarm_{uid}", f".Lcold_{uid}:"] + prologue_dma(dt) + [f".Lwarm_{uid}:"]
+    else:
+        out += prologue_dma(dt)
     out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(dt, 2, QK, False)
     # reference max of tile 0 (S in buffer A), masked in place
     out += ["s_nop 7", "s_nop 7", "s_nop 3"]
@@ -594,7 +629,10 @@ def main_loop(dt, uid):
 def epilogue(dt, uid):
     # epilogue: normalise, O rows (16-byte stores after a permlane32 exchange), LSE
     out = [f".Lexit_{uid}:"]
-    out += ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_nop 7", "s_nop 7", "s_nop 3"]
+    out += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    if WARM:
+        out += ["s_barrier"] + warm_issue(uid)
+    out += ["s_nop 7", "s_nop 7", "s_nop 3"]
     if PS:
         # temps and the offsets (from their AGPR operands) in S buffer A above the store sets
         inv, L, t, lse, cls, pinf = (f"v{56 + i}" for i in range(6))
@@ -742,7 +780,14 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[loff0] "v"(loff0)', '[loff1] "v"(loff1)']
 
 
+WARM_SIG = ", const int kblo2, const int kbhi2, const int kvb2, const int warm, const int nxt"
+WARM_OPS = ['[kblo2] "s"(kblo2)', '[kbhi2] "s"(kbhi2)', '[kvb2] "s"(kvb2)', '[warm] "s"(warm)',
+            '[nxt] "s"(nxt)']
+
+
 def ops():
+    if WARM:
+        return OPS + WARM_OPS
     if not PS:
         return OPS
     av = ("lim0", "lim1", "qoff0", "qoff1", "ooff0", "ooff1", "loff0", "loff1")
@@ -757,6 +802,7 @@ def emit(out=OUT):
         "// The 4-wave D = 128 forward's item body (fmha_fwd4_kernel.h): one asm statement with a",
         "// fixed register map; see the generator's docstring for the map and the schedule.",
         "#pragma once",
+        f"#define XFA_FWD4_WARM {1 if WARM else 0}",
         '#include "fmha_common.h"',
         "",
         "namespace xfa {",
@@ -765,7 +811,7 @@ def emit(out=OUT):
     ]
     for dt in ("bf16", "f16"):
         prog = item_program_ps(dt) if PS else item_program(dt)
-        lines.append(f"__device__ __forceinline__ void fwd4_item_{dt}({SIG}) {{")
+        lines.append(f"__device__ __forceinline__ void fwd4_item_{dt}({SIG}{WARM_SIG if WARM else ''}) {{")
         lines.append("    asm volatile(")
         for b in prog:
             lines.append(f'        "{b}\\n"')
@@ -790,10 +836,12 @@ if __name__ == "__main__":
     ap.add_argument("--nvpre", type=int, default=NVPRE, help="next-step V^T frags read early")
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
     ap.add_argument("--dma2h", action="store_true", help="DMA after the barrier, half a step more lead")
+    ap.add_argument("--warm", action="store_true", help="warm start: the next item's K_0, K_1 in the tail")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     set_mode(a.ps)
     KS, VS, READ_LEAD, NPRE, NVPRE = a.ks, a.vs, a.lead, a.npre, a.nvpre
     ABL = set(x for x in a.abl.split(",") if x)
     DMA2H = a.dma2h
+    WARM = a.warm
     emit(a.out)

@@ -7,4 +7,4 @@ if [ $e -eq 0 ]; then
 fi
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r4_suite1.log 2>&1; e=$?; tail -5 gpurun_out/r4_suite1.log
 if [ $e -gt 1 ]; then exit $e; fi
-timeout -k 10 200 python tools/lib_ab.py variants/lib_base.so variants/lib_k8.so variants/lib_k8incr.so --rounds 7 > gpurun_out/ab_k8incr_c.log 2>&1 && grep -E "fwd" gpurun_out/ab_k8incr_c.log && timeout -k 10 200 python tools/lib_ab.py variants/lib_base.so variants/lib_k8.so variants/lib_k8incr.so --rounds 5 --noncausal > gpurun_out/ab_k8incr_nc.log 2>&1 && grep fwd gpurun_out/ab_k8incr_nc.log
+timeout -k 10 200 python tools/lib_ab.py variants/lib_k8incr.so variants/lib_warm.so --rounds 7 > gpurun_out/ab_warm_c.log 2>&1 && grep -E "fwd|check" gpurun_out/ab_warm_c.log && timeout -k 10 200 python tools/lib_ab.py variants/lib_k8incr.so variants/lib_warm.so --rounds 5 --noncausal > gpurun_out/ab_warm_nc.log 2>&1 && grep -E "fwd|check" gpurun_out/ab_warm_nc.log
