@@ -107,7 +107,18 @@ int fmha_last_num_splits(void);
  * scores with the same state drop the same entries (flash-attn's rng_state = {seed, offset}). */
 void fmha_set_rng_state(uint64_t seed, uint64_t offset);
 
-/* Library version / build identification, e.g. "xf-fmha-gfx950 2.1".  2.0 (round 3) changed
+/* Graph-capturable dropout key (ABI 2.2): the next dropout call on this thread reads its key
+ * on the device when it runs - seed = *seed_ptr, offset = *offset_ptr + offset_add (torch's
+ * philox_cuda_state under stream capture: seed_.ptr, offset_.ptr, offset_intragraph_, which the
+ * reference unpacks in its kernels, flash_api_hip.cpp:509) - and a forward writes the key it used
+ * to rng_out[0..1] (device int64 x 2, may be NULL; the reference's params.rng_state).  The
+ * backward of that forward: fmha_set_rng_state_device(rng_out, rng_out + 1, 0, NULL).
+ * seed_ptr == NULL keeps the host key of fmha_set_rng_state (rng_out still receives it).
+ * One-shot: consumed by the next call with p_dropout > 0 (fmha_set_rng_state clears it too). */
+void fmha_set_rng_state_device(const int64_t* seed_ptr, const int64_t* offset_ptr,
+                               uint64_t offset_add, int64_t* rng_out);
+
+/* Library version / build identification, e.g. "xf-fmha-gfx950 2.2".  2.0 (round 3) changed
  * argument lists of existing symbols; 2.1 exports those under _v2 names (see INTEGRATION.md
  * "ABI history"). */
 const char* fmha_version(void);

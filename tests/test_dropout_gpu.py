@@ -153,3 +153,53 @@ def test_dropout_deterministic_bwd_bitwise(xfa):
     assert torch.equal(o1, o2)
     for a, b_ in zip(g1, g2):
         assert torch.equal(a, b_)
+
+
+def test_dropout_graph_capture(xfa):
+    """Dropout inside a captured HIP graph (the key comes from torch's philox_cuda_state, read on
+    the device): every replay draws a fresh mask, the device rng_state the forward
+    writes is the key it used (the CPU Philox of that key reproduces the mask bit for bit), and
+    the backward captured with that rng_state regenerates the same mask (dK / dV equal an eager
+    backward given the same key; dQ differs by atomic summation order only)."""
+    torch.manual_seed(4)
+    b, h, hk, sq, sk, d, p = 1, 2, 2, 128, 160, 64, 0.17
+    q = torch.randn(b, sq, h, d, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(b, sk, hk, d, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(b, sk, hk, d, device=DEV, dtype=torch.bfloat16)
+    dout = torch.randn(b, sq, h, d, device=DEV, dtype=torch.bfloat16)
+    sc = d ** -0.5
+
+    def bwd(out, lse, rng):
+        return xfa.paged_attn.bwd(dout, q, k, v, out, lse, None, None, None, None, p, sc, True,
+                                  -1, -1, 0.0, False, None, rng)
+
+    def step():
+        r = xfa.paged_attn.fwd(q, k, v, None, None, p, sc, True, -1, -1, 0.0, True, None)
+        out, lse, s, rng = r[0], r[5], r[6], r[7]
+        g = bwd(out, lse, rng)
+        return out, lse, s, rng, g[0], g[1], g[2]
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out, lse, s, rng, dq, dk, dv = step()
+    keys, masks = [], []
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        seed, offset = (int(x) for x in rng.tolist())
+        kept = ~torch.signbit(s[:, :, :sq, :sk].float()).cpu()
+        assert torch.equal(kept, torch.from_numpy(drf.keep_mask(seed, offset, b, h, sq, sk, p)))
+        e = bwd(out, lse, rng.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(e[1], dk) and torch.equal(e[2], dv)
+        assert (e[0].float() - dq.float()).abs().max().item() <= 1e-2 * dq.float().abs().max().item()
+        keys.append((seed, offset))
+        masks.append(kept)
+    assert keys[0] != keys[1]
+    assert not torch.equal(masks[0], masks[1])

@@ -46,6 +46,7 @@ _SIGS = {
     "fmha_last_num_splits": [],
     "fmha_version": [],
     "fmha_set_rng_state": [C.c_uint64, C.c_uint64],
+    "fmha_set_rng_state_device": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "fmha_set_option": [C.c_char_p, C.c_int],
     "fmha_get_option": [C.c_char_p],
 }

@@ -223,6 +223,12 @@ void dense_strides(FwdParams& p, int sq, int sk, int h, int hk, int d) {
 // Dropout RNG state of the calling thread (fmha_set_rng_state); read by every forward /
 // backward call with p_dropout > 0.
 thread_local uint64_t g_seed = 0, g_offset = 0;
+// fmha_set_rng_state_device: the key read on the device (graph capture), and where a forward
+// writes the key it used
+thread_local const int64_t* g_seed_ptr = nullptr;
+thread_local const int64_t* g_offset_ptr = nullptr;
+thread_local uint64_t g_offset_add = 0;
+thread_local int64_t* g_rng_out = nullptr;
 
 template <typename P>
 bool set_dropout(P& p, float p_dropout, float softcap) {
@@ -235,7 +241,13 @@ bool set_dropout(P& p, float p_dropout, float softcap) {
     p.keep_thr = (uint32_t)std::floor(keep * 255.0);
     p.rp_keep = 1.f / keep;
     p.seed = g_seed;
-    p.offset = g_offset;
+    p.offset = g_seed_ptr ? g_offset_add : g_offset;
+    p.seed_ptr = g_seed_ptr;
+    p.offset_ptr = g_offset_ptr;
+    p.rng_out = g_rng_out;
+    // the device key is one-shot: a later call cannot write through a stale rng_out
+    g_seed_ptr = g_offset_ptr = nullptr;
+    g_rng_out = nullptr;
     return true;
 }
 
@@ -330,9 +342,22 @@ extern "C" {
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
-const char* fmha_version(void) { return "xf-fmha-gfx950 2.1"; }
+const char* fmha_version(void) { return "xf-fmha-gfx950 2.2"; }
 
-void fmha_set_rng_state(uint64_t seed, uint64_t offset) { g_seed = seed; g_offset = offset; }
+void fmha_set_rng_state(uint64_t seed, uint64_t offset) {
+    g_seed = seed;
+    g_offset = offset;
+    g_seed_ptr = g_offset_ptr = nullptr;
+    g_rng_out = nullptr;
+}
+
+void fmha_set_rng_state_device(const int64_t* seed_ptr, const int64_t* offset_ptr, uint64_t offset_add,
+                               int64_t* rng_out) {
+    g_seed_ptr = (seed_ptr && offset_ptr) ? seed_ptr : nullptr;
+    g_offset_ptr = g_seed_ptr ? offset_ptr : nullptr;
+    g_offset_add = offset_add;
+    g_rng_out = rng_out;
+}
 
 int fmha_set_option(const char* name, int value) {
     clear_error();

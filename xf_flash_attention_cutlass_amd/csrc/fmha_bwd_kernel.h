@@ -173,6 +173,8 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
     constexpr int KT_BYTES = BN * HD * 2;
     constexpr int QT_BYTES = BQ * HD * 2;
     constexpr int NDQ = (HD / 16) / (NW / 2);   // 16x16 dQ tiles per wave (2 query halves)
+    uint64_t dseed = 0, doff = 0;                // dropout key (fmha_common.h drop_key)
+    if (FEAT && p.drop) drop_key(p, dseed, doff);
     constexpr int QLD = BQ * CPR / NT;          // Q (and dO) chunks per thread
     static_assert(QLD >= 1 && BQ * CPR == QLD * NT, "Q/dO tile geometry");
 
@@ -462,7 +464,7 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
                 // dropout: the 4 rows pos0 .. +3 of this lane's key are one Philox block
                 // (fmha_common.h drop_block, the forward's draw); kept P scaled by 1 / p_keep
                 u32x4 dw = u32x4{0, 0, 0, 0};
-                if (FEAT && p.drop) dw = drop_block(p.seed, p.offset, bidx * p.h + head, pos0, my_key[ks]);
+                if (FEAT && p.drop) dw = drop_block(dseed, doff, bidx * p.h + head, pos0, my_key[ks]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int r = 4 * gq + i;

@@ -152,6 +152,12 @@ struct FwdParams {
     uint32_t keep_thr;
     float rp_keep;
     uint64_t seed, offset;
+    // graph-capturable key (fmha_set_rng_state_device): seed = *seed_ptr, offset = *offset_ptr
+    // + offset, read on the device at run time; rng_out (forward): the key used, written back
+    // for the backward as the reference's kernel writes params.rng_state
+    const int64_t* seed_ptr;
+    const int64_t* offset_ptr;
+    int64_t* rng_out;
 };
 
 struct CombineParams {
@@ -208,6 +214,12 @@ struct BwdParams {
     uint32_t keep_thr;
     float rp_keep;
     uint64_t seed, offset;
+    // graph-capturable key (fmha_set_rng_state_device): seed = *seed_ptr, offset = *offset_ptr
+    // + offset, read on the device at run time; rng_out (forward): the key used, written back
+    // for the backward as the reference's kernel writes params.rng_state
+    const int64_t* seed_ptr;
+    const int64_t* offset_ptr;
+    int64_t* rng_out;
 };
 
 // ------------------------------------------------------------------ dropout RNG --
@@ -236,6 +248,17 @@ __device__ __forceinline__ u32x4 drop_block(const uint64_t seed, const uint64_t 
                                             const int pos, const int key) {
     return philox4x32_7((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32),
                         (uint32_t)key >> 2, (uint32_t)pos >> 2, (uint32_t)bh, (uint32_t)offset);
+}
+// The launch's Philox key: the host values, or (graph capture) the generator's device state, as
+// the reference unpacks philox_cuda_state in its kernels (at::cuda::philox::unpack).
+template <typename P>
+__device__ __forceinline__ void drop_key(const P& p, uint64_t& seed, uint64_t& offset) {
+    seed = p.seed;
+    offset = p.offset;
+    if (p.seed_ptr) {
+        seed = (uint64_t)*p.seed_ptr;
+        offset = (uint64_t)*p.offset_ptr + p.offset;
+    }
 }
 __device__ __forceinline__ bool drop_keep(const uint32_t word, const int j, const uint32_t thr) {
     return ((word >> (8 * j)) & 0xFFu) <= thr;

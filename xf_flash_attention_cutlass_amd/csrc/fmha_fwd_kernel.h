@@ -299,11 +299,13 @@ __device__ __forceinline__ void fwd_item(const FwdParams& p, char* smem, const i
     auto drop_tile = [&](V8 (&pb)[4], const int n0) {
         if (!(FEAT && p.drop)) return;
         const int bhg = bidx * p.h + head;
+        uint64_t dseed, doff;
+        drop_key(p, dseed, doff);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const u32x4 w = drop_block(p.seed, p.offset, bhg, pos, n0 + 32 * kt + 8 * j + 4 * hh);
+                const u32x4 w = drop_block(dseed, doff, bhg, pos, n0 + 32 * kt + 8 * j + 4 * hh);
                 const uint32_t word = (pos & 2) ? ((pos & 1) ? w[3] : w[2]) : ((pos & 1) ? w[1] : w[0]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -800,6 +802,15 @@ __global__ void __launch_bounds__(NW * 64, fwd_waves_per_simd(HD)) fmha_fwd_kern
             m_block = gridDim.y - 1 - blockIdx.y;
         }
         fwd_item<HD, T, NW, MASK, FEAT>(p, smem, bh, m_block, blockIdx.z);
+    }
+    // the key this launch used, for the backward (the reference writes params.rng_state the
+    // same way, flash_fwd_kernel_hip.h); one lane of one workgroup
+    if (FEAT && p.drop && p.rng_out && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 &&
+        threadIdx.x == 0) {
+        uint64_t dseed, doff;
+        drop_key(p, dseed, doff);
+        p.rng_out[0] = (int64_t)dseed;
+        p.rng_out[1] = (int64_t)doff;
     }
     // dynamic queue: every workgroup has made its last (failed) claim when it gets here; the
     // last one to finish resets the counters for the next launch on this stream

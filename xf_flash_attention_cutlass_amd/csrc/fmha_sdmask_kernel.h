@@ -35,6 +35,8 @@ __global__ void __launch_bounds__(256) fmha_sdmask_kernel(const FwdParams p, T* 
         ? p.lse[(int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos] * 1.4426950408889634f
         : 0.f;
     const float alibi_w = p.alibi ? p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul : 0.f;
+    uint64_t dseed, doff;
+    drop_key(p, dseed, doff);
     for (int key = threadIdx.x; key < sk_r; key += blockDim.x) {
         float val = 0.f;
         if (pos < sq && key < sk) {
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(256) fmha_sdmask_kernel(const FwdParams p, T* 
                 if (p.alibi) w -= alibi_w * (float)abs(pos + diag - key);
                 pr = exp2f(w * p.scale_log2 - lse2);
             }
-            const u32x4 blk = drop_block(p.seed, p.offset, bidx * p.h + head, pos, key);
+            const u32x4 blk = drop_block(dseed, doff, bidx * p.h + head, pos, key);
             const bool keep = !p.drop || drop_keep(blk[pos & 3], key & 3, p.keep_thr);
             val = keep ? pr : -pr;
         }

@@ -85,27 +85,49 @@ at::Tensor alibi_for_c(c10::optional<at::Tensor>& a, int b, int h, int64_t* bstr
     return s;
 }
 
-// Dropout: seed / offset from torch's HIP generator (flash-attn's philox_cuda_state use,
-// export.cpp:616-627), handed to the C ABI's thread RNG state; returned as rng_state
-// (int64 [2] on the host: the backward reads it without a device round trip).
-at::Tensor dropout_rng(float p_dropout, c10::optional<at::Generator>& gen_, int64_t counter_offset) {
-    uint64_t seed = 0, offset = 0;
+// Dropout: the key from torch's HIP generator as philox_cuda_state (export.cpp:616-627,
+// flash_api_hip.cpp:509): outside stream capture the host seed / offset; under capture the
+// generator's device seed / offset pointers, read by the kernels when the graph runs (so every
+// replay draws a fresh mask).  rng_state is an int64 [2] on q's device, as upstream returns it;
+// the forward kernel writes the key it used into it, and the backward reads it on the device.
+at::Tensor dropout_rng(float p_dropout, c10::optional<at::Generator>& gen_, int64_t counter_offset,
+                       const at::Device& dev) {
+    auto rng = torch::empty({2}, torch::dtype(torch::kInt64).device(dev));
     if (p_dropout > 0.f) {
         auto gen = at::get_generator_or_default<at::CUDAGeneratorImpl>(gen_, at::cuda::detail::getDefaultCUDAGenerator());
-        std::lock_guard<std::mutex> lock(gen->mutex_);
-        auto so = gen->philox_engine_inputs((uint64_t)counter_offset);
-        seed = so.first;
-        offset = so.second;
+        at::PhiloxCudaState st;
+        {
+            std::lock_guard<std::mutex> lock(gen->mutex_);
+            st = gen->philox_cuda_state((uint64_t)counter_offset);
+        }
+        if (st.captured_) {
+            fmha_set_rng_state(0, 0);
+            fmha_set_rng_state_device(st.seed_.ptr, st.offset_.ptr, st.offset_intragraph_, rng.data_ptr<int64_t>());
+        } else {
+            fmha_set_rng_state(st.seed_.val, st.offset_.val);
+            fmha_set_rng_state_device(nullptr, nullptr, 0, rng.data_ptr<int64_t>());
+        }
+    } else {
+        fmha_set_rng_state(0, 0);
     }
-    fmha_set_rng_state(seed, offset);
-    return torch::tensor({(int64_t)seed, (int64_t)offset}, torch::dtype(torch::kInt64));
+    return rng;
 }
 
+// The backward's key: a device rng_state (the forward's) is read on the device (capturable);
+// a host one (a caller's own {seed, offset}) is passed by value.
 void dropout_rng_restore(float p_dropout, c10::optional<at::Tensor>& rng_state) {
     if (p_dropout <= 0.f) return;
     TORCH_CHECK(rng_state.has_value(), "backward with dropout needs the forward's rng_state");
-    auto r = rng_state.value().to(torch::kCPU).to(torch::kInt64).contiguous();
-    TORCH_CHECK(r.numel() == 2, "rng_state must hold {seed, offset}");
+    const at::Tensor& r0 = rng_state.value();
+    TORCH_CHECK(r0.numel() == 2 && r0.scalar_type() == torch::kInt64, "rng_state must be int64 {seed, offset}");
+    if (r0.is_cuda()) {
+        TORCH_CHECK(r0.is_contiguous(), "rng_state must be contiguous");
+        const int64_t* d = r0.data_ptr<int64_t>();
+        fmha_set_rng_state(0, 0);
+        fmha_set_rng_state_device(d, d + 1, 0, nullptr);
+        return;
+    }
+    auto r = r0.contiguous();
     fmha_set_rng_state((uint64_t)r.data_ptr<int64_t>()[0], (uint64_t)r.data_ptr<int64_t>()[1]);
 }
 
@@ -169,7 +191,7 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     auto opts = q.options();
     auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, seqlen_q, seqlen_k);
-    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32);
+    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32, q.device());
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
 
@@ -282,7 +304,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     auto opts = q.options();
     auto softmax_lse = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, max_seqlen_q, max_seqlen_k);
-    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32);
+    auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32, q.device());
     if (zero_tensors) {
         out.zero_();
         softmax_lse.fill_(-std::numeric_limits<float>::infinity());
