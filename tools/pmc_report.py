@@ -11,8 +11,9 @@
 Derivations (MI355X_MICROARCH.md):
   * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8;
     effective clock = cycles / dispatch duration (reads high for dispatches < ~0.3 ms);
-  * v_mfma_f32_32x32x16 (and the fp8 32x32x64 scaled form at 2x the K) hold one SIMD's matrix
-    pipe for 32 cycles, 16x16x32 for 16: MFMA utilisation = SQ_INSTS_MFMA x 32 / (4 SIMDs x
+  * v_mfma_f32_32x32x16 holds one SIMD's matrix pipe for 32 cycles, 16x16x32 for 16, the
+    block-scaled fp8 v_mfma_scale_f32_32x32x64_f8f6f4 for 64 (twice the bf16 form's cycles at 4x
+    the K; the fp8 kernels issue only that one): MFMA utilisation = SQ_INSTS_MFMA x 32 (64) / (4 SIMDs x
     CUs x cycles) - an upper bound for kernels that also issue 16x16x32 (the backward's dQ);
   * FETCH_SIZE reports half the bytes of wide streaming reads on gfx950: x2; WRITE_SIZE exact
     for 16-B/lane stores and float atomics; both in KiB;
@@ -99,7 +100,8 @@ def main():
                 e["profiled_duration_us"] = round(dur / 1e3, 2)
                 e["effective_clock_ghz"] = round(cyc / dur, 3)
             if cyc and "SQ_INSTS_MFMA" in c:
-                e["mfma_util_from_insts"] = round(c["SQ_INSTS_MFMA"] * 32 / (4 * NUM_CUS * cyc), 4)
+                per = 64 if "fp8" in k or "fwd8" in k else 32
+                e["mfma_util_from_insts"] = round(c["SQ_INSTS_MFMA"] * per / (4 * NUM_CUS * cyc), 4)
             if c.get("SQ_INSTS_MFMA"):
                 e["valu_per_mfma"] = round(c.get("SQ_INSTS_VALU", 0) / c["SQ_INSTS_MFMA"], 2)
                 e["lds_insts_per_mfma"] = round(c.get("SQ_INSTS_LDS", 0) / c["SQ_INSTS_MFMA"], 2)
