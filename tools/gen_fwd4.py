@@ -298,6 +298,8 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
         else:
             g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
+    # one piece per gap: a gap's M0 writes all precede its loads below
+    assert all(len(v) == 1 for v in dma_gap.values()), "two LDS-DMA pieces in one gap"
     # the previous step's prefetch of this step's first K / V^T fragments, in issue order
     issued, last_idx = [], {}
     for w, f in prefetch_order():

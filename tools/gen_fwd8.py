@@ -289,11 +289,20 @@ def step_body(ph, kind, mask, vm=NDMA):
             if not (smby.get(g) or dma_gap.get(g) or rby.get(g)):
                 continue
             body.append("s_nop 0")
+        # a gap's DMA pieces: each load right behind its own M0 (the first pair straddles the
+        # gap's softmax ops, later ones an s_nop for the SALU M0 write -> LDS-DMA hazard).  The
+        # short (8-MFMA) prologue steps place two pieces in one gap: emitting both M0 writes
+        # before both loads sent the first piece to the second's LDS address.
         dm = dma_gap.get(g, [])
-        body += [dma(w, i)[0] for w, i in dm]
+        if dm:
+            body.append(dma(*dm[0])[0])
         for seq, txt in sorted(smby.get(g, []), key=lambda x: x[0]):
             body += txt
-        body += [dma(w, i)[1] for w, i in dm]
+        if dm:
+            body.append(dma(*dm[0])[1])
+            for w, i in dm[1:]:
+                a, b = dma(w, i)
+                body += [a, "s_nop 0", b]
         issue_reads(g, body)
         out += body
     return out
