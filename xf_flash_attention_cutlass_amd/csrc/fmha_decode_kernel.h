@@ -134,6 +134,23 @@ __device__ __forceinline__ bool dec_slot(const FwdParams& p, const int f, const 
     return true;
 }
 
+// Decode image for D = 128 with the 16-row tile (dec_mr 16).  Lane l reads K row l % 16 at
+// chunk 4s + l / 16 (ds_read_b128: lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) and
+// V^T rows 4 (l / 16) + (l % 16) / 4 of its 32-lane half (ds_read_b64_tr_b16); the forward's
+// swz<128> (built for the 32-row tile's lane map) put two lanes of every such group on one bank —
+// half of the decode's LDS cycles were conflicts (r03b PMC).  This map is conflict-free for both:
+// a K group's 16 (row, chunk) pairs need f(rows 4..11) closed under ^1, a V half's 8 rows need
+// distinct f(row) >> 1 — rows 0-7 -> 2r, rows 8-11 -> the odd partners of rows 4-7, rows 12-15 ->
+// those of rows 0-3 (period 16 rows).
+__device__ __forceinline__ int dswz16(int row) {
+    const int r = row & 15;
+    return r < 8 ? 2 * r : (r < 12 ? 2 * r - 7 : 2 * r - 23);
+}
+template <int HD, int MR> __device__ __forceinline__ int dec_off(int row, int chunk) {
+    if constexpr (HD == 128 && MR == 16) return row * (HD * 2) + ((chunk ^ dswz16(row)) << 4);
+    else return lds_off<HD>(row, chunk);
+}
+
 template <int HD, typename T, bool KV8, int MR, int NWV = kDecWaves>
 __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParams p) {
     using V8 = typename DT<T>::v8;
@@ -303,12 +320,12 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
 #pragma unroll
     for (int i = 0; i < NLD; ++i)
 #pragma unroll
-        for (int h2 = 0; h2 < 3 - ESZ; ++h2) kw[i][h2] = lds_off<HD>(RPI * i + lrow, (3 - ESZ) * lch + h2);
+        for (int h2 = 0; h2 < 3 - ESZ; ++h2) kw[i][h2] = dec_off<HD, MR>(RPI * i + lrow, (3 - ESZ) * lch + h2);
     // K operand (A of S^T) of k-step s: row lr (key), 16-byte chunk s KS/8 + hh; the second
     // 16-key block (MR = 16) is 16 rows on, same swizzle (the swizzle has period 16)
     int koff[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) koff[s] = lds_off<HD>(lr, (KS / 8) * s + hh);
+    for (int s = 0; s < NS; ++s) koff[s] = dec_off<HD, MR>(lr, (KS / 8) * s + hh);
     // V^T operand (A of O^T) through ds_read_b64_tr_b16: a 16-lane group reads a 4-key x
     // 16-column block and each lane receives its column's 4 keys
     const int q4 = (lane & 15) >> 2;
@@ -320,11 +337,11 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
             if constexpr (MR == 32) {
                 const int r = 4 * hh + q4 + 8 * part;
                 const int col = 32 * dt + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-                voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+                voff[part][dt] = dec_off<HD, MR>(r, col >> 3) + 8 * ((col >> 2) & 1);
             } else {
                 const int r = 4 * hh + q4 + 16 * part;  // keys 4g.. and 16+4g.. of the tile
                 const int col = 16 * dt + 4 * (lane & 3);
-                voff[part][dt] = lds_off<HD>(r, col >> 3) + 8 * ((col >> 2) & 1);
+                voff[part][dt] = dec_off<HD, MR>(r, col >> 3) + 8 * ((col >> 2) & 1);
             }
         }
 
