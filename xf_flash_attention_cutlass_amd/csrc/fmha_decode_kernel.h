@@ -141,13 +141,16 @@ __device__ __forceinline__ bool dec_slot(const FwdParams& p, const int f, const 
 // half of the decode's LDS cycles were conflicts (r03b PMC).  This map is conflict-free for both:
 // a K group's 16 (row, chunk) pairs need f(rows 4..11) closed under ^1, a V half's 8 rows need
 // distinct f(row) >> 1 — rows 0-7 -> 2r, rows 8-11 -> the odd partners of rows 4-7, rows 12-15 ->
-// those of rows 0-3 (period 16 rows).
+// those of rows 0-3 (period 16 rows).  Chunks 8-15 also swap within their ^1 pairs (c ^ c[3]): a
+// fp8 dequant store writes the 8 even (or odd) chunks of one row from an 8-lane group, which the
+// 32-bank store path saw as 4 slots twice; now 8 (uniform per read instruction, so the reads keep
+// their property).  Bank-checked for every instruction of the loop in tools/decode_banks.py.
 __device__ __forceinline__ int dswz16(int row) {
     const int r = row & 15;
     return r < 8 ? 2 * r : (r < 12 ? 2 * r - 7 : 2 * r - 23);
 }
 template <int HD, int MR> __device__ __forceinline__ int dec_off(int row, int chunk) {
-    if constexpr (HD == 128 && MR == 16) return row * (HD * 2) + ((chunk ^ dswz16(row)) << 4);
+    if constexpr (HD == 128 && MR == 16) return row * (HD * 2) + ((chunk ^ ((chunk >> 3) & 1) ^ dswz16(row)) << 4);
     else return lds_off<HD>(row, chunk);
 }
 
