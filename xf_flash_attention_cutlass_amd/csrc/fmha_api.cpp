@@ -307,6 +307,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     p.dec_slots = p.dec_bal ? p.b * splits : 0;
     p.dec_cap = p.dec_bal ? std::min(p.dec_slots, 128) : 0;
     p.dec_ns = nullptr;
+    p.comb_row = o.comb_row.load();
     const int ext = p.dec_bal ? p.dec_cap : splits;   // split extent of the scratch
     if (splits > 1) {
         const int hd = hd_bucket(p.d);
@@ -374,7 +375,7 @@ int fmha_set_option(const char* name, int value) {
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 1},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
         {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
-        {"fp8_w4", &o.fp8_w4, 0, 1},
+        {"fp8_w4", &o.fp8_w4, 0, 1},           {"comb_row", &o.comb_row, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;
@@ -399,6 +400,7 @@ int fmha_get_option(const char* name) {
     XFA_GET(fwd_order) XFA_GET(fwd_dyn) XFA_GET(fwd_xcdq) XFA_GET(fwd_pipe) XFA_GET(fwd_decode)
     XFA_GET(dec_wg_per_cu) XFA_GET(dec_hmaj) XFA_GET(dec_mr) XFA_GET(fwd_w4)
     XFA_GET(bwd_order) XFA_GET(bwd_desc) XFA_GET(dec_fold) XFA_GET(dec_bal) XFA_GET(fp8_w4)
+    XFA_GET(comb_row)
 #undef XFA_GET
     fail(1, "unknown option '%s'", name);
     return -1;

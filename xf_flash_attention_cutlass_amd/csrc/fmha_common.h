@@ -145,6 +145,7 @@ struct FwdParams {
     int xcdq;                  // dynamic queue kind (1 per-XCD queues)
     int device;                // current device id (per-device one-time kernel attributes)
     int fwd4;                  // 1: the 4-wave D = 128 forward where eligible (fmha_fwd4_kernel.h)
+    int comb_row;              // split combine: one workgroup per row when rows are few
     // dropout (flash_fwd_kernel_hip.h's Dropout, dropout_hip.h:14-109): keep a score iff its
     // Philox byte <= keep_thr (= floor(p_keep * 255), paged_attn.cpp:106-113); kept P scaled by
     // rp_keep = 1 / p_keep.  drop = 0: no dropout.

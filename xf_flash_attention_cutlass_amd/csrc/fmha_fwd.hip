@@ -27,7 +27,8 @@ typedef _Float16 elem_t;
 #endif
 
 static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
-                                 void (*kern)(const CombineParams)) {
+                                 void (*kern)(const CombineParams),
+                                 void (*row_kern)(const CombineParams) = nullptr) {
     CombineParams cp;
     cp.oaccum = p.oaccum;
     cp.lseaccum = p.lseaccum;
@@ -39,6 +40,12 @@ static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
     cp.num_splits = p.num_splits;
     cp.dec_ns = p.decode && p.dec_bal ? p.dec_ns : nullptr;
     const int64_t crow = (int64_t)p.b * p.h * p.seqlen_q;
+    const int ext = cp.dec_ns ? p.dec_cap : p.num_splits;
+    // few rows (the decode shapes): one workgroup per row, all of its partials in flight at once
+    if (row_kern && p.comb_row && ext <= 128 && crow <= 8 * (int64_t)p.num_cus) {
+        hipLaunchKernelGGL(row_kern, dim3((unsigned)crow), dim3(256), 0, st, cp);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
     return hipGetLastError();
 }
@@ -79,7 +86,8 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (p.dec_ctr) return hipSuccess;          // the last split of each (b, kv head) merged
-    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
+    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>,
+                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr);
 }
 
 template <int HD, typename T, int NW>
@@ -116,7 +124,8 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
-    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>);
+    return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>,
+                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr);
 }
 
 #if XFA_HD == 128

@@ -885,4 +885,83 @@ __global__ void __launch_bounds__(256) fmha_combine_kernel(const CombineParams c
         cp.lse[(int64_t)bidx * cp.lse_batch + (int64_t)head * cp.lse_head + pos] = lse;
 }
 
+// Split-KV combine, one workgroup per row (few rows: the decode shapes, where the per-wave kernel
+// above leaves most CUs idle and waits one memory latency per batch of 8 splits).  Thread t owns
+// float4 chunk t % (HD / 4) of the splits s = t / (HD / 4) (mod 256 / (HD / 4)): every partial
+// row of the first 8 rounds is loaded before the LSE merge (wave 0, splits across lanes) has
+// produced the weights, so the row costs about one memory latency; the 256 / (HD / 4) partial
+// sums of a chunk meet in LDS.  HD in {64, 128, 256}, at most 128 splits.
+template <int HD, typename T>
+__global__ void __launch_bounds__(256) fmha_combine_row_kernel(const CombineParams cp) {
+    constexpr int D4 = HD / 4;
+    constexpr int G = 256 / D4;
+    constexpr int NB = 8;
+    static_assert(G * D4 == 256, "chunks per thread");
+    __shared__ float wsh[128];
+    __shared__ f32x4 red[G][D4];
+    const int t = threadIdx.x;
+    const int64_t rid = blockIdx.x;
+    const int64_t rows = (int64_t)cp.b * cp.h * cp.seqlen_q;
+    const int pos = (int)(rid % cp.seqlen_q);
+    const int head = (int)((rid / cp.seqlen_q) % cp.h);
+    const int bidx = (int)(rid / ((int64_t)cp.seqlen_q * cp.h));
+    const int ns = cp.dec_ns ? cp.dec_ns[bidx] : cp.num_splits;
+    const int c = t % D4, g = t / D4;
+    const float* oa = cp.oaccum + rid * HD + 4 * c;
+    const int64_t sstride = rows * HD;
+    f32x4 x[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int sp = g + G * u;
+        x[u] = sp < ns ? *reinterpret_cast<const f32x4*>(oa + sp * sstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (t < 64) {
+        const float l0 = t < ns ? cp.lseaccum[t * rows + rid] : -INFINITY;
+        const float l1 = t + 64 < ns ? cp.lseaccum[(t + 64) * rows + rid] : -INFINITY;
+        float mx = wave_max_halves(fmaxf(l0, l1));
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        float sum = mx == -INFINITY ? 0.f : __expf(l0 - mx) + __expf(l1 - mx);
+        sum = wave_sum_halves(sum);
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+        const bool empty = (mx == -INFINITY) || sum == 0.f;
+        const float lse = empty ? INFINITY : __logf(sum) + mx;
+        wsh[t] = empty ? 0.f : __expf(l0 - lse);
+        wsh[t + 64] = empty ? 0.f : __expf(l1 - lse);
+        if (cp.lse && t == 0) cp.lse[(int64_t)bidx * cp.lse_batch + (int64_t)head * cp.lse_head + pos] = lse;
+    }
+    __syncthreads();
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int sp = g + G * u;
+        if (sp < ns) acc += wsh[sp] * x[u];
+    }
+    for (int s0 = g + G * NB; s0 < ns; s0 += G * NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int sp = s0 + G * u;
+            x[u] = sp < ns ? *reinterpret_cast<const f32x4*>(oa + sp * sstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int sp = s0 + G * u;
+            if (sp < ns) acc += wsh[sp] * x[u];
+        }
+    }
+    red[g][c] = acc;
+    __syncthreads();
+    if (t < D4) {
+        f32x4 o = red[0][t];
+#pragma unroll
+        for (int i = 1; i < G; ++i) o += red[i][t];
+        T* orow = reinterpret_cast<T*>(cp.o) + (int64_t)bidx * cp.o_batch + (int64_t)pos * cp.o_row +
+                  (int64_t)head * cp.o_head;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (4 * t + i < cp.d) orow[4 * t + i] = (T)o[i];
+    }
+}
+
 }  // namespace xfa

@@ -29,6 +29,7 @@ struct Options {
     std::atomic<int> dec_wg_per_cu{2};   // decode split target: workgroups per CU over all (b, kv head)
     std::atomic<int> dec_mr{16};         // decode MFMA rows: 16 when the query rows fit 16 (C5: 105 vs
                                          // 110 us with dec_hmaj = 1), else 32
+    std::atomic<int> comb_row{1};        // split combine: one workgroup per row when rows are few
     std::atomic<int> dec_fold{0};        // decode: the last split of each (b, kv head) merges the partials
     std::atomic<int> dec_bal{1};         // decode over per-sequence cache lengths (2 <= b <= 64): split
                                          // slots shared in proportion to the key tiles (ragged caches)
