@@ -354,8 +354,10 @@ def test_decode_kernel_dense(xfa, sq, h, hk, d, causal, dtype):
 @pytest.mark.parametrize("sq,h,hk", [(1, 32, 8), (3, 12, 1), (2, 64, 2)])
 def test_decode_folded_combine_bitexact(xfa, sq, h, hk):
     """dec_fold=1 (the last split of each (b, kv head) merges the partials in the decode
-    launch) gives the same output and LSE as the separate combine kernel, bit for bit, twice
-    in a row (the split counters reset themselves)."""
+    launch) gives the same output and LSE as the separate per-wave combine kernel
+    (comb_row=0: the same serial order over splits), bit for bit, twice in a row (the split
+    counters reset themselves); the default one-workgroup-per-row combine (comb_row=1) sums
+    the splits in groups, equal up to fp32 reassociation."""
     from xf_flash_attention_cutlass_amd import capi
     L = capi.lib()
     torch.manual_seed(8)
@@ -363,7 +365,14 @@ def test_decode_folded_combine_bitexact(xfa, sq, h, hk):
     q = torch.randn(b, sq, h, d, dtype=torch.bfloat16).to(DEV)
     k = torch.randn(b, sk, hk, d, dtype=torch.bfloat16).to(DEV)
     v = torch.randn(b, sk, hk, d, dtype=torch.bfloat16).to(DEV)
-    base = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    row = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    assert L.fmha_set_option(b"comb_row", 0) == 0
+    try:
+        base = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
+    finally:
+        L.fmha_set_option(b"comb_row", 1)
+    assert (row[0].float() - base[0].float()).abs().max().item() <= 1e-2
+    assert (row[1] - base[1]).abs().max().item() <= 1e-5
     assert L.fmha_set_option(b"dec_fold", 1) == 0
     try:
         for _ in range(2):

@@ -44,11 +44,11 @@ def run(lib, name, q, k, v, causal):
     out = torch.full((b, sq, h, d), 7.0, device="cuda", dtype=torch.bfloat16)
     lse = torch.full((b, h, sq), 7.0, device="cuda")
     qd, kd, vd = qq.cuda(), kk.cuda(), vv.cuda()
-    rc = lib.fmha_fwd_fp8(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), lse.data_ptr(),
+    lib.fmha_fwd_fp8(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), lse.data_ptr(),
                           qs, ks, vs, sq, sk, b, h, hk, d, d ** -0.5, -1, 0 if causal else -1, False,
                           capi.stream_handle())
     torch.cuda.synchronize()
-    assert rc == 0, lib.fmha_last_error()
+    assert lib.fmha_last_status() == 0, lib.fmha_last_error()
     ro, rl = ref_attn(qq.float() * qs, kk.float() * ks, vv.float() * vs, causal)
     o = out.float().cpu()
     l = lse.cpu()
