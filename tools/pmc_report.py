@@ -69,6 +69,16 @@ def trace_median_ns(d, kernel):
     return ds[len(ds) // 2] if ds else None
 
 
+def stats_run_line(root, m):
+    """The bench JSON line the profiled stats run itself printed (same process as the kernel
+    trace: its ms_per_step is the step the trace's kernel median belongs to)."""
+    f = os.path.join(root, f"{m}_stats.out")
+    if not os.path.exists(f):
+        return None
+    lines = [x for x in open(f) if x.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "")[:120]
 
@@ -120,7 +130,9 @@ def main():
                 e["hbm_bytes_per_launch"] = int(rd + wr)
             e["counters_mean"] = {x: round(v, 1) for x, v in sorted(c.items()) if not x.startswith("__")}
             res[short(k)] = e
+        line = stats_run_line(root, m)
         pmc[m] = {"dominant_kernel": short(dom["Name"]) if dom else None,
+                  "stats_run_ms_per_step": line["ms_per_step"] if line else None,
                   "dominant_avg_ns": float(dom["AverageNs"]) if dom else None,
                   "dominant_median_ns": med,
                   "dominant_calls": int(dom["Calls"]) if dom else None,
@@ -129,6 +141,7 @@ def main():
             key = next((k for k in res if k == short(dom["Name"])), None)
             if key and "hbm_bytes_per_launch" in res[key]:
                 traffic[m] = {"kernel": key, "avg_ns": float(dom["AverageNs"]), "median_ns": med,
+                              "stats_run_ms_per_step": line["ms_per_step"] if line else None,
                               "calls": int(dom["Calls"]),
                               "hbm_bytes_per_launch": res[key]["hbm_bytes_per_launch"],
                               "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + "
