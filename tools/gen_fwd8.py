@@ -379,22 +379,6 @@ def redo_block(par, uid):
     return out
 
 
-def redo_check(par, uid, tag):
-    return [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
-            f"v_cmp_lt_f32_e64 s[{SCM}:{SCM + 1}], %[thr], v{LT + 1}",
-            f"s_or_b64 vcc, vcc, s[{SCM}:{SCM + 1}]",
-            "s_nop 1",
-            f"s_cbranch_vccz .Lnr{tag}_{uid}",
-            f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
-            f".Lpc{tag}_{uid}:",
-            f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
-            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, 0",
-            f"s_branch .Lredo{par}_{uid}",
-            f".Lnr{tag}_{uid}:",
-            f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}",
-            f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-
-
 def item_program(dt, uid="%="):
     out = ["s_waitcnt lgkmcnt(0)"]
     out += [f"v_mov_b32 v{PINF}, 0x7f800000", f"v_mov_b32 v{NINF}, 0xff800000",
@@ -442,7 +426,10 @@ def item_program(dt, uid="%="):
 
 
 def main_loop(uid):
+    """per phase the unmasked step falls through into the next phase; the masked and idle steps
+    and the redo stubs live after the loop and branch back (gen_fwd4.py main_loop_ff)"""
     out = [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
+    tail = []
     for ph in range(4):
         par = ph & 1
         out.append(f".Lph{ph}_{uid}:")
@@ -451,19 +438,41 @@ def main_loop(uid):
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         out += step_body(ph, QK | SM | PV, False)
-        out += redo_check(par, uid, f"u{ph}")
-        out.append(f"s_branch .Lnx{ph}_{uid}")
-        out.append(f".Lm{ph}_{uid}:")
-        out += step_body(ph, QK | SM | PV, True)
-        out += redo_check(par, uid, f"m{ph}")
-        out.append(f"s_branch .Lnx{ph}_{uid}")
-        out.append(f".Li{ph}_{uid}:")
-        out += step_body(ph, 0, False)
+        inl, stub = redo_check_ff(par, uid, f"u{ph}")
+        out += inl
+        tail += stub
         out.append(f".Lnx{ph}_{uid}:")
         out += [f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
                 f"s_cbranch_scc1 .Lexit_{uid}"]
+        tail.append(f".Lm{ph}_{uid}:")
+        tail += step_body(ph, QK | SM | PV, True)
+        inl, stub = redo_check_ff(par, uid, f"m{ph}")
+        tail += inl + [f"s_branch .Lnx{ph}_{uid}"] + stub
+        tail.append(f".Li{ph}_{uid}:")
+        tail += step_body(ph, 0, False)
+        tail.append(f"s_branch .Lnx{ph}_{uid}")
     out.append(f"s_branch .Lph0_{uid}")
-    return out
+    return out + tail
+
+
+def redo_check_ff(par, uid, tag):
+    """redo_check with the common case falling through (a not-taken branch to an out-of-line
+    stub that sets the return address); returns (inline part, stub)"""
+    inline = [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
+              f"v_cmp_lt_f32_e64 s[{SCM}:{SCM + 1}], %[thr], v{LT + 1}",
+              f"s_or_b64 vcc, vcc, s[{SCM}:{SCM + 1}]",
+              "s_nop 1",
+              f"s_cbranch_vccnz .Lrc{tag}_{uid}",
+              f".Lnr{tag}_{uid}:",
+              f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}",
+              f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
+    stub = [f".Lrc{tag}_{uid}:",
+            f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
+            f".Lpc{tag}_{uid}:",
+            f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
+            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, 0",
+            f"s_branch .Lredo{par}_{uid}"]
+    return inline, stub
 
 
 def epilogue(dt, uid):
