@@ -466,11 +466,13 @@ def redo_check_ff(par, uid, tag):
               f".Lnr{tag}_{uid}:",
               f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}",
               f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
+    # the return point lies BEFORE the stub: a negative offset, so the high word adds its sign
+    # extension (-1) with the carry
     stub = [f".Lrc{tag}_{uid}:",
             f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
             f".Lpc{tag}_{uid}:",
             f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
-            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, 0",
+            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",
             f"s_branch .Lredo{par}_{uid}"]
     return inline, stub
 
