@@ -9,7 +9,11 @@
 #pragma once
 
 #include "fmha_common.h"
+#ifdef XFA_FWD8_BODY                     // A/B builds of a generated variant (tools/fwd8_variant.py)
+#include XFA_FWD8_BODY
+#else
 #include "fmha_fwd8_body.h"
+#endif
 
 namespace xfa {
 
