@@ -53,11 +53,7 @@ TMP, NTMP = 160, 16
 LT, LIM, NM, LRUN = 176, 178, 180, 182
 MISC = 184
 SC127, PINF, NINF = 189, 190, 191
-NVFIX = 198
-# row-sum partial accumulators: LTX[rb][k] takes the scores with (v mod 32) mod 4 == k, so the
-# four adds of one MFMA gap are independent (one chain per row block serialised them); the four
-# are summed into LTX[rb][0] = v{LT + rb} before the redo test
-LTX = [[176, 192, 194, 196], [177, 193, 195, 197]]
+NVFIX = 192
 ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 160, 224
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94
 SKR, SVR = 80, 84
@@ -139,11 +135,10 @@ def sm_value_ops(v, src_buf, dst_buf, mask, seq=False):
     if mask:
         ex += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}", f"v_cndmask_b32 {t}, 0, {t}, vcc"]
     ops.append((1, ex))
-    acc = LTX[rb][(v % 32) % 4]
-    if v % 32 < 4:
-        ops.append((2, [f"v_mov_b32 v{acc}, {t}"]))
+    if v % 32 == 0:
+        ops.append((2, [f"v_mov_b32 v{LT + rb}, {t}"]))
     else:
-        ops.append((2, [f"v_add_f32 v{acc}, v{acc}, {t}"]))
+        ops.append((2, [f"v_add_f32 v{LT + rb}, v{LT + rb}, {t}"]))
     if v & 1:
         tp = f"v{TMP + (v - 1) % NTMP}"
         pd = f"v{PBASE[dst_buf] + dword}"
@@ -380,7 +375,6 @@ def redo_block(par, uid):
         out.append("s_nop 1")
         out += softmax_block(sc_buf, pn_buf, rb * 32, rb * 32 + 32)
         out.append("s_nop 1")
-        out += lt_combine((rb,))
     out += ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
     return out
 
@@ -424,7 +418,6 @@ def item_program(dt, uid="%="):
                 f"v_cmp_lg_f32 vcc, v{NINF}, {mx}",
                 f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
     out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(3, QK | SM, False)
-    out += lt_combine()
     out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
     out += main_loop(uid)
     out += redo_block(0, uid) + redo_block(1, uid)
@@ -462,22 +455,10 @@ def main_loop(uid):
     return out + tail
 
 
-def lt_combine(rbs=(0, 1)):
-    """the tile row sums: LTX[rb][0] += the other three partial accumulators"""
-    out = []
-    for rb in rbs:
-        x = LTX[rb]
-        out += [f"v_add_f32 v{x[0]}, v{x[0]}, v{x[1]}", f"v_add_f32 v{x[2]}, v{x[2]}, v{x[3]}"]
-    for rb in rbs:
-        x = LTX[rb]
-        out.append(f"v_add_f32 v{x[0]}, v{x[0]}, v{x[2]}")
-    return out
-
-
 def redo_check_ff(par, uid, tag):
     """redo_check with the common case falling through (a not-taken branch to an out-of-line
     stub that sets the return address); returns (inline part, stub)"""
-    inline = lt_combine() + [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
+    inline = [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
               f"v_cmp_lt_f32_e64 s[{SCM}:{SCM + 1}], %[thr], v{LT + 1}",
               f"s_or_b64 vcc, vcc, s[{SCM}:{SCM + 1}]",
               "s_nop 1",
