@@ -58,6 +58,7 @@ ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 160, 224
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94
 SKR, SVR = 80, 84
 NDMA = 4              # LDS-DMA wave-instructions per step (2 K + 2 V pieces)
+ABL = set()           # timing ablations of the main-loop steps (results INVALID): nodma nosm nobar nolgkm
 
 QK, SM, PV = 1, 2, 4
 MNEM = "v_mfma_scale_f32_32x32x64_f8f6f4"
@@ -227,9 +228,10 @@ def step_body(ph, kind, mask, vm=NDMA):
         return [f"s_add_u32 m0, %[kdst], {base + i * 1024}",
                 f"buffer_load_dwordx4 {op}, {srd}, 0 offen lds"]
 
-    dmas = [(w, i) for i in range(2) for w in ("K", "V")]
+    main = bool(kind & PV)                    # a main-loop step (ablations touch only those)
+    dmas = [] if ("nodma" in ABL and main) else [(w, i) for i in range(2) for w in ("K", "V")]
     sm = []
-    if kind & SM:
+    if kind & SM and not ("nosm" in ABL and main):
         span = G if G else 16
         for v in range(64):
             tg = (v * span) // 64
@@ -280,11 +282,12 @@ def step_body(ph, kind, mask, vm=NDMA):
             nd = need[g]
             if nd in last_idx and last_idx[nd] >= waited:
                 n = min(len(issued) - last_idx[nd] - 1, 15)
-                body.append(f"s_waitcnt lgkmcnt({n})")
+                if not ("nolgkm" in ABL and main):
+                    body.append(f"s_waitcnt lgkmcnt({n})")
                 waited = len(issued) - n
             body.append(mfma[g])
             if g == mid:
-                body += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
+                body += [] if ("nobar" in ABL and main) else [f"s_waitcnt vmcnt({vm})", "s_barrier"]
         else:
             if not (smby.get(g) or dma_gap.get(g) or rby.get(g)):
                 continue
@@ -569,4 +572,10 @@ def emit(out=OUT):
 
 
 if __name__ == "__main__":
-    emit()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
+    ap.add_argument("--out", default=OUT)
+    a = ap.parse_args()
+    ABL = set(x for x in a.abl.split(",") if x)
+    emit(a.out)

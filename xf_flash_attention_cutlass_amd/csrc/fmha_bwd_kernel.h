@@ -66,10 +66,18 @@ template <> struct DT16<_Float16> {
 
 enum { kLsdPermute = 0, kLsdVec = 1, kLsdScalar = 2 };
 
-// dS^T tile [256 keys][32 q] bf16, 64-byte rows: XOR the 16-byte chunk with bit 3 of the row
-// so the two 4-row blocks one tr-read half touches (8 rows apart) use different banks.
+// dS^T tile [256 keys][32 q] bf16, 64-byte rows, 8-byte pieces of 4 q.  The tr reads of dQ
+// (two 4-row blocks 8 rows apart per 32-lane half) need rows r and r + 8 on different 16-byte
+// chunk pairs: the chunk takes row bit 3 in its bit 1.  The dS^T stores (ds_write_b64, 16
+// lanes = 16 consecutive rows at one column, 32 banks) need the 16 pieces on 16 different
+// 8-byte slots of the 128-byte bank window: row bit 0 is the address' bit 6, and rows bits 1-3
+// pick the chunk's bit 0 (bit 1), its bit 1 (bit 3) and the piece within the chunk (bit 2).
+// (Round 3's image flipped the chunk by bit 3 only: 4-way conflicts on every store, 11.9 % of
+// the backward's LDS cycles; tools/bwd_banks.py.)
 __device__ __forceinline__ int ds_off(int row, int col) {
-    return row * 64 + ((((col >> 3) ^ (((row >> 3) & 1) << 1))) << 4) + ((col >> 2) & 1) * 8;
+    const int s1 = (((row >> 3) & 1) << 1) | ((row >> 1) & 1);
+    const int s0 = (row >> 2) & 1;
+    return row * 64 + (((col >> 3) ^ s1) << 4) + ((((col >> 2) & 1) ^ s0) << 3);
 }
 
 // ---------------------------------------------------------------- preprocess ---------------
