@@ -14,9 +14,12 @@ tools/probe_fp8.hip):
                                                         ds_read_b64_tr_b8 (32 keys of d column)
   DMA K_{j+4}, V_{j+2} into 4-slot LDS rings             4 LDS-DMA pieces of 1 KiB per wave
 
-P leaves the S^T accumulator with keys 32 kt + 8 d + 4 hh + 0..3 in dword d of key half kt; two
-v_cvt_pk_fp8_f32 pack a dword, and one v_permlane32_swap per dword pair regroups (kt = 0, 1) so
-lane half h holds keys 32 h .. 32 h + 31 in order: the B operand of PV (fmha_fwd_fp8_kernel.h).
+P leaves the S^T accumulator with keys 32 kt + 8 d + 4 hh + i (i = 0..3) in the lane half hh;
+two v_cvt_pk_fp8_f32 pack them into P dword 4 kt + d, which is directly the B operand of PV with
+its k index permuted: k slot (h, byte j) is key 32 (j >> 4) + 8 ((j >> 2) & 3) + 4 h + (j & 3).
+The V^T reads apply the same permutation (a ds_read_b64_tr_b8 takes each of its 8 rows from
+its own lane's address: read kb, row b is key 16 kb + 8 (b >> 2) + 4 h + (b & 3)), so P needs
+no cross-lane regroup (round 3's kernel paid one v_permlane32_swap per dword pair).
 Softmax as the bf16 body: no row max in the loop (P against tile 0's true max, a tile whose
 partial row sum passes 2^slack takes the rare rescale path; slack <= 8 keeps P <= 256 < 448, the
 e4m3 maximum), c = softmax_scale log2(e) q_scale k_scale, O scaled by v_scale / l at the end.
@@ -103,10 +106,10 @@ def vtup(slot, kb=None):
 
 
 def value_info(v):
-    """score v: rb, kt, r, key offset within the tile minus 4 hh, P dword (pre-swap), byte"""
+    """score v: rb, kt, r, key offset within the tile minus 4 hh, P dword"""
     rb, kt, r = v // 32, (v // 16) % 2, v % 16
     off = 32 * kt + 8 * (r >> 2) + (r & 3)
-    dword = rb * 8 + 2 * (r >> 2) + kt
+    dword = rb * 8 + 4 * kt + (r >> 2)
     return rb, kt, r, off, dword
 
 
@@ -125,10 +128,8 @@ def mfma_order(kind):
 
 
 def sm_value_ops(v, src_buf, dst_buf, mask, seq=False):
-    """softmax ops of score v: [(stage, [texts])]; stage 0 fma, 1 exp (+mask), 2 add + cvt,
-    4 the dword pair's permlane32 swap (after the kt = 1 half of the dword is packed; two gaps
-    on, so the swap's 2 wait states after the cvt are met; seq: a plain sequence, explicit
-    s_nop)"""
+    """softmax ops of score v: [(stage, [texts])]; stage 0 fma, 1 exp (+mask), 2 add + cvt
+    (seq: a plain sequence)"""
     rb, kt, r, off, dword = value_info(v)
     t = f"v{TMP + v % NTMP}"
     ops = [(0, [f"v_fma_f32 {t}, {se(src_buf, v)}, %[c], v{NM + rb}"])]
@@ -145,10 +146,6 @@ def sm_value_ops(v, src_buf, dst_buf, mask, seq=False):
         pd = f"v{PBASE[dst_buf] + dword}"
         sel = " op_sel:[0,0,1]" if (r & 3) == 3 else ""
         ops.append((2, [f"v_cvt_pk_fp8_f32 {pd}, {tp}, {t}{sel}"]))
-    if kt == 1 and (r & 3) == 3:
-        d = r >> 2
-        a, b = PBASE[dst_buf] + rb * 8 + 2 * d, PBASE[dst_buf] + rb * 8 + 2 * d + 1
-        ops.append((4, (["s_nop 1"] if seq else []) + [f"v_permlane32_swap_b32 v{a}, v{b}"]))
     return ops
 
 
@@ -201,7 +198,7 @@ def step_body(ph, kind, mask, vm=NDMA):
             g = min(max(vlast.get(dt - 4, -3) + 2 if dt >= 4 else 0, vfirst[dt] - READ_LEAD, 0),
                     vfirst[dt] - 1)
             for kb in range(4):
-                reads.append((g, kb, f"ds_read_b64_tr_b8 {vtup(dt, kb)}, %[va{dt}] offset:{vro + kb * 1024}",
+                reads.append((g, kb, f"ds_read_b64_tr_b8 {vtup(dt, kb)}, %[va{dt}] offset:{vro + kb * 2048}",
                               ("V", dt)))
     gprev = mid + 1
     npar = (par + 1) & 1
@@ -215,7 +212,7 @@ def step_body(ph, kind, mask, vm=NDMA):
         else:
             lo = max(mid + 1, (vlast[f] + 2) if (kind & PV) else 0)
             g = max(lo, gprev)
-            txt = [f"ds_read_b64_tr_b8 {vtup(f, kb)}, %[va{f}] offset:{vno + kb * 1024}"
+            txt = [f"ds_read_b64_tr_b8 {vtup(f, kb)}, %[va{f}] offset:{vno + kb * 2048}"
                    for kb in range(4)]
         gprev = g = min(g, G)
         for i, t in enumerate(txt):

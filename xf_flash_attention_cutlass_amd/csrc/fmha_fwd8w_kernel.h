@@ -34,7 +34,11 @@ __device__ __forceinline__ i32x4 fwd8w_srd(const void* base, uint32_t bytes) {
 
 // fp8 LDS images (fmha_fwd_fp8_kernel.h): XOR of the 16-byte chunk by the row
 __device__ __forceinline__ int k8w_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
-__device__ __forceinline__ int v8w_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ (((row >> 1) & 3) << 1)); }
+// V: the transposed reads take rows 4h + {0..3, 8..11} (+ 16 kb) per lane half h (the P
+// k permutation, tools/gen_fwd8.py): the chunk XOR uses row bits 1 and 3 so the 8 rows of
+// one read half land on 4 different chunk pairs per row parity (conflict-free)
+__device__ __forceinline__ int v8w_swz(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
+__device__ __forceinline__ int v8w_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ v8w_swz(row)); }
 
 // One (batch x kv head, 256-row query block) item.
 template <bool F16>
@@ -127,7 +131,7 @@ __device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const
         const int g = wave * 2 + i;
         const int r = 8 * g + (lane >> 3);
         dk[i] = r * k_row + 16 * ((lane & 7) ^ ((r >> 1) & 7));
-        dv[i] = r * v_row + 16 * ((lane & 7) ^ (((r >> 1) & 3) << 1));
+        dv[i] = r * v_row + 16 * ((lane & 7) ^ v8w_swz(r));
     }
     const int sbase = (int)(size_t)smem;
     int ka[4], va[4];
@@ -137,7 +141,7 @@ __device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const
         for (int u = 0; u < 2; ++u) ka[2 * s + u] = sbase + k8w_off(lr, 4 * s + 2 * hh + u);
     {
         const int i = lane & 15, q = i >> 1, pb8 = i & 1, g = (lane >> 4) & 1;
-        const int r = 32 * hh + q;
+        const int r = 4 * hh + (q & 3) + 8 * (q >> 2);   // read kb adds 16 kb rows
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) va[dt] = sbase + kFwd8wVReg + v8w_off(r, 2 * dt + g) + 8 * pb8;
     }
