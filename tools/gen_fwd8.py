@@ -61,6 +61,8 @@ ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 160, 224
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94
 SKR, SVR = 80, 84
 NDMA = 4              # LDS-DMA wave-instructions per step (2 K + 2 V pieces)
+LEAD2 = False         # DMA one more step ahead: step j issues K_{j+5}, V_{j+3} (the 4-slot rings
+                      # allow it) and the mid-point wait keeps two steps' pieces in flight
 ABL = set()           # timing ablations of the main-loop steps (results INVALID): nodma nosm nobar nolgkm
 
 QK, SM, PV = 1, 2, 4
@@ -155,7 +157,7 @@ def prefetch_order():
     return [("N", f) for f in range(4)] + [("W", dt) for dt in range(NWPRE)]
 
 
-def step_body(ph, kind, mask, vm=NDMA):
+def step_body(ph, kind, mask, vm=None):
     """instructions of one step at ring phase ph (= j mod 4)"""
     par = ph & 1
     sn_buf, sc_buf = (0, 1) if par == 0 else (1, 0)      # S_{j+2} -> sn, scores of j+1 in sc
@@ -164,8 +166,10 @@ def step_body(ph, kind, mask, vm=NDMA):
     vro = (ph & 3) * TILE                                # V_j
     kno = ((ph + 3) & 3) * TILE                          # K_{j+3}: the next step's frags
     vno = ((ph + 1) & 3) * TILE                          # V_{j+1}: the next step's first frags
-    kdo = (ph & 3) * TILE                                # K_{j+4} (DMA)
-    vdo = VREG + ((ph + 2) & 3) * TILE                   # V_{j+2} (DMA)
+    if vm is None:
+        vm = 2 * NDMA if LEAD2 else NDMA
+    kdo = ((ph + (1 if LEAD2 else 0)) & 3) * TILE       # K_{j+4} (LEAD2: K_{j+5}) (DMA)
+    vdo = VREG + ((ph + (3 if LEAD2 else 2)) & 3) * TILE  # V_{j+2} (LEAD2: V_{j+3}) (DMA)
     kslot = lambda f, p: 4 * (p & 1) + f                 # noqa: E731
 
     mf = mfma_order(kind)
@@ -316,8 +320,9 @@ def step_prep(incr=False):
             out += [f"s_add_u32 s{r}, s{r}, %[kstep]", f"s_addc_u32 s{r + 1}, s{r + 1}, 0",
                     f"s_sub_i32 s{r + 2}, s{r + 2}, %[kstep]", f"s_max_i32 s{r + 2}, s{r + 2}, 0"]
         return out
-    out = [f"s_add_i32 s{ST}, s{SJ}, 4", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
-           f"s_add_i32 s{ST}, s{SJ}, 2", f"s_max_i32 s{ST}, s{ST}, 0",
+    kl, vl = (5, 3) if LEAD2 else (4, 2)
+    out = [f"s_add_i32 s{ST}, s{SJ}, {kl}", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
+           f"s_add_i32 s{ST}, s{SJ}, {vl}", f"s_max_i32 s{ST}, s{ST}, 0",
            f"s_mul_i32 s{SVO}, s{ST}, %[kstep]"]
     for r, lo, hi, off in ((SKR, "kblo", "kbhi", SKO), (SVR, "vblo", "vbhi", SVO)):
         out += [f"s_add_u32 s{r}, %[{lo}], s{off}", f"s_addc_u32 s{r + 1}, %[{hi}], 0",
@@ -397,9 +402,12 @@ def item_program(dt, uid="%="):
         out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
     # prologue: j = -4, -3 DMA only (K_0, K_1; the K_0 frags read at -3's end); j = -2 QK(0);
     # tile 0's row max; j = -1 QK(1) + SM(0); then the loop
+    if LEAD2:
+        # j = -5 .. -3 DMA only (K_0 .. K_2, V_0); Q and K_0 landed at -3's wait (vmcnt 8)
+        out += [f"s_mov_b32 s{SJ}, -5"] + step_prep() + step_body(3, 0, False)
     out += [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(0, 0, False)
     out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(1, 0, False)
-    out += [f"s_waitcnt vmcnt({NDMA})"]        # Q landed (older than j = -3's DMA)
+    out += [f"s_waitcnt vmcnt({2 * NDMA if LEAD2 else NDMA})"]   # Q landed (older than the DMA in flight)
     out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(2, QK, False)
     out += ["s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"]
     mx, t2 = f"v{MISC}", f"v{MISC + 1}"
@@ -572,7 +580,13 @@ if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
+    ap.add_argument("--lead2", action="store_true", help="DMA one more step ahead")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     ABL = set(x for x in a.abl.split(",") if x)
+    LEAD2 = a.lead2
+    if LEAD2:
+        # V_{j+3} overwrites V_{j-1}'s slot in step j's first half, before its mid barrier: every
+        # V^T fragment of a tile must then be read in the previous step (none after a barrier)
+        NWPRE = 4
     emit(a.out)
