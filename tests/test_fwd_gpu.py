@@ -157,6 +157,42 @@ def test_fwd_split_kv_matches_single_pass(xfa, splits):
     assert (outs[0][0].float() - outs[1][0].float()).abs().max().item() < 2e-3
 
 
+@pytest.mark.parametrize("d,splits,causal", [(64, 100, False), (128, 100, True), (256, 37, False),
+                                             (128, 5, True)])
+def test_split_combine_row_kernel(xfa, d, splits, causal):
+    """The one-workgroup-per-row combine (comb_row=1, few rows) against the per-wave combine
+    (comb_row=0) and the single pass: splits past the first 64-split batch of its loop, D = 64 /
+    128 / 256, and causal rows that see no key of the last splits (empty partials, LSE -inf)."""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    torch.manual_seed(11)
+    b, h, sq, sk = 1, 2, 40, 6500
+    q = torch.randn(b, sq, h, d, dtype=torch.bfloat16, device=DEV)
+    k = torch.randn(b, sk, h, d, dtype=torch.bfloat16, device=DEV)
+    v = torch.randn(b, sk, h, d, dtype=torch.bfloat16, device=DEV)
+    outs = {}
+    for name, s, cr in (("single", 1, 1), ("row", splits, 1), ("wave", splits, 0)):
+        assert L.fmha_set_option(b"comb_row", cr) == 0
+        try:
+            o = torch.empty_like(q)
+            lse = torch.empty(b, h, sq, device=DEV)
+            L.fmha_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), None, sq, sk, b, h,
+                       h, d, 0.0, capi.stream_handle(), None, d ** -0.5, None, lse.data_ptr(), -1,
+                       0 if causal else -1, 0.0, False, False, s)
+            capi.check()
+            if s > 1:
+                assert L.fmha_last_num_splits() == s
+        finally:
+            L.fmha_set_option(b"comb_row", 1)
+        torch.cuda.synchronize()
+        outs[name] = (o.float(), lse)
+    (o1, l1), (o2, l2), (o3, l3) = outs["single"], outs["row"], outs["wave"]
+    assert (o2 - o3).abs().max().item() <= 1e-2 * o3.abs().max().item()
+    assert (l2 - l3).abs().max().item() <= 1e-5
+    assert (o2 - o1).abs().max().item() <= 2e-2
+    assert (l2 - l1).abs().max().item() <= 1e-4
+
+
 def test_fwd_sq_gt_sk_causal_empty_rows(xfa):
     """Bottom-right causal alignment: with sq > sk the first sq-sk rows see no key -> O = 0,
     LSE = +inf (flash_fwd_kernel_hip.h:626-670)."""
