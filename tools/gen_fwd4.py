@@ -64,6 +64,7 @@ NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's s
 ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
+EPI_IDLE = False      # a wave's epilogue runs in its first idle step (causal diagonal)
 FF = True             # fall-through loop layout (masked / idle steps and redo stubs out of line;
                       # round 4, same box: +0.9 % causal, +0.2 % non-causal, bit-identical)
 
@@ -652,7 +653,10 @@ def main_loop_ff(dt, uid):
     """main loop, fall-through layout: per phase the unmasked step runs straight into the next
     phase (no taken branch on the common path); the masked and idle steps and the redo stubs live
     after the loop and branch back"""
-    out = [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
+    out = [f"s_mov_b32 s{SJ}, 0"]
+    if EPI_IDLE:
+        out.append(f"s_mov_b32 s{SKO}, 0")          # (SKO is the prologue's temp) rows not stored
+    out += [f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
     tail = []
     for ph in range(4):
         par = ph & 1
@@ -675,8 +679,21 @@ def main_loop_ff(dt, uid):
         tail += inl + [f"s_branch .Lnx{ph}_{uid}"] + stub
         tail.append(f".Li{ph}_{uid}:")
         tail += step_body(dt, ph, 0, False)
-        tail.append(f"s_branch .Lnx{ph}_{uid}")
+        if EPI_IDLE:
+            # first idle step (after its barrier): the rows' epilogue, once
+            tail += [f"s_cmp_eq_u32 s{SKO}, 0", f"s_cbranch_scc0 .Lnx{ph}_{uid}",
+                     f"s_mov_b32 s{SKO}, 1",
+                     f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
+                     f".Lpe{ph}_{uid}:",
+                     f"s_add_u32 s{SRA}, s{SRA}, .Lnx{ph}_{uid} - .Lpe{ph}_{uid}",
+                     # (.Lnx lies before this stub: negative offset, high word + -1 + carry)
+                     f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",
+                     f"s_branch .Lepi_{uid}"]
+        else:
+            tail.append(f"s_branch .Lnx{ph}_{uid}")
     out.append(f"s_branch .Lph0_{uid}")
+    if EPI_IDLE:
+        tail += epilogue_idle(dt, uid)
     return out + tail
 
 
@@ -714,7 +731,27 @@ def epilogue(dt, uid):
     out += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
     if WARM:
         out += ["s_barrier"] + warm_issue(uid)
+    if EPI_IDLE:
+        # a wave that went idle before the last step has stored its rows already
+        out += [f"s_cmp_eq_u32 s{SKO}, 1", f"s_cbranch_scc1 .Lend_{uid}"]
     out += ["s_nop 7", "s_nop 7", "s_nop 3"]
+    out += epilogue_core(dt)
+    if EPI_IDLE:
+        out.append(f".Lend_{uid}:")
+    return out
+
+
+def epilogue_idle(dt, uid):
+    """EPI_IDLE: the epilogue as a routine for the first idle step of a wave (its rows have no
+    key tile left: O and the row sums are final), entered with the return address in SRA, so
+    its row stores leave while the workgroup's last waves still compute and the item's tail
+    holds only their stores"""
+    return ([f".Lepi_{uid}:", "s_nop 7", "s_nop 7", "s_nop 3"] + epilogue_core(dt) +
+            [f"s_setpc_b64 s[{SRA}:{SRA + 1}]"])
+
+
+def epilogue_core(dt):
+    out = []
     if PS:
         # temps and the offsets (from their AGPR operands) in S buffer A above the store sets
         inv, L, t, lse, cls, pinf = (f"v{56 + i}" for i in range(6))
@@ -920,6 +957,7 @@ if __name__ == "__main__":
     ap.add_argument("--dma2h", action="store_true", help="DMA after the barrier, half a step more lead")
     ap.add_argument("--warm", action="store_true", help="warm start: the next item's K_0, K_1 in the tail")
     ap.add_argument("--no-ff", dest="ff", action="store_false", help="the branch-around loop layout")
+    ap.add_argument("--epi-idle", action="store_true", help="epilogue in the first idle step")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     set_mode(a.ps)
@@ -928,4 +966,6 @@ if __name__ == "__main__":
     DMA2H = a.dma2h
     WARM = a.warm
     FF = a.ff
+    EPI_IDLE = a.epi_idle
+    assert not (EPI_IDLE and (PS or WARM or not FF)), "--epi-idle: fall-through layout, no PS / warm"
     emit(a.out)
