@@ -48,7 +48,7 @@ TILE = 64 * 128       # bytes of one fp8 K (or V) tile
 VREG = 4 * TILE       # V ring after the K ring (LDS)
 QK_LEAD = 2           # QK MFMAs before the first PV MFMA
 READ_LEAD = 4         # gaps an LDS read leads the MFMA that consumes it (at least)
-NWPRE = 3             # V^T frags of the next step read in this step's second half
+NWPRE = 4             # V^T frags of the next step read in this step's second half (all: LEAD2)
 
 SBASE = (0, 64)
 PBASE = (128, 144)
@@ -61,7 +61,7 @@ ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 160, 224
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94
 SKR, SVR = 80, 84
 NDMA = 4              # LDS-DMA wave-instructions per step (2 K + 2 V pieces)
-LEAD2 = False         # DMA one more step ahead: step j issues K_{j+5}, V_{j+3} (the 4-slot rings
+LEAD2 = True          # DMA one more step ahead: step j issues K_{j+5}, V_{j+3} (the 4-slot rings
                       # allow it) and the mid-point wait keeps two steps' pieces in flight
 ABL = set()           # timing ablations of the main-loop steps (results INVALID): nodma nosm nobar nolgkm
 
@@ -580,13 +580,13 @@ if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
-    ap.add_argument("--lead2", action="store_true", help="DMA one more step ahead")
+    ap.add_argument("--no-lead2", dest="lead2", action="store_false",
+                    help="DMA two steps ahead only (3 V^T fragments prefetched)")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     ABL = set(x for x in a.abl.split(",") if x)
     LEAD2 = a.lead2
-    if LEAD2:
-        # V_{j+3} overwrites V_{j-1}'s slot in step j's first half, before its mid barrier: every
-        # V^T fragment of a tile must then be read in the previous step (none after a barrier)
-        NWPRE = 4
+    # LEAD2: V_{j+3} overwrites V_{j-1}'s slot in step j's first half, before its mid barrier, so
+    # every V^T fragment of a tile must be read in the previous step (none after a barrier)
+    NWPRE = 4 if LEAD2 else 3
     emit(a.out)
