@@ -427,16 +427,17 @@ def item_program(dt, uid="%="):
                 f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
     out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(3, QK | SM, False)
     out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-    out += main_loop(uid)
+    out += main_loop(uid, dt)
     out += redo_block(0, uid) + redo_block(1, uid)
     out += epilogue(dt, uid)
     return out
 
 
-def main_loop(uid):
+def main_loop(uid, dt):
     """per phase the unmasked step falls through into the next phase; the masked and idle steps
     and the redo stubs live after the loop and branch back (gen_fwd4.py main_loop_ff)"""
-    out = [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
+    out = [f"s_mov_b32 s{SJ}, 0", f"s_mov_b32 s{SKO}, 0",      # SKO: rows stored (EPI_IDLE)
+           f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
     tail = []
     for ph in range(4):
         par = ph & 1
@@ -458,9 +459,16 @@ def main_loop(uid):
         tail += inl + [f"s_branch .Lnx{ph}_{uid}"] + stub
         tail.append(f".Li{ph}_{uid}:")
         tail += step_body(ph, 0, False)
-        tail.append(f"s_branch .Lnx{ph}_{uid}")
+        # first idle step (after its barrier): the rows' epilogue, once
+        tail += [f"s_cmp_eq_u32 s{SKO}, 0", f"s_cbranch_scc0 .Lnx{ph}_{uid}",
+                 f"s_mov_b32 s{SKO}, 1",
+                 f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
+                 f".Lpe{ph}_{uid}:",
+                 f"s_add_u32 s{SRA}, s{SRA}, .Lnx{ph}_{uid} - .Lpe{ph}_{uid}",
+                 f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",     # (.Lnx lies before: negative offset)
+                 f"s_branch .Lepi_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
-    return out + tail
+    return out + tail + epilogue_idle(uid, dt)
 
 
 def redo_check_ff(par, uid, tag):
@@ -486,9 +494,22 @@ def redo_check_ff(par, uid, tag):
 
 
 def epilogue(dt, uid):
-    """O = v_scale O / l as 16-byte rows of the output dtype (permlane32 exchange), LSE"""
-    out = [f".Lexit_{uid}:", "s_waitcnt vmcnt(0) lgkmcnt(0)", "s_nop 7", "s_nop 7", "s_nop 7",
-           "s_nop 7", "s_nop 3"]
+    """O = v_scale O / l as 16-byte rows of the output dtype (permlane32 exchange), LSE; skipped
+    by a wave that stored its rows in its first idle step (gen_fwd4.py EPI_IDLE)"""
+    return ([f".Lexit_{uid}:", "s_waitcnt vmcnt(0) lgkmcnt(0)",
+             f"s_cmp_eq_u32 s{SKO}, 1", f"s_cbranch_scc1 .Lend_{uid}",
+             "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"] + epilogue_core(dt) +
+            [f".Lend_{uid}:"])
+
+
+def epilogue_idle(uid, dt):
+    """the epilogue as a routine for a wave's first idle step (return address in SRA)"""
+    return ([f".Lepi_{uid}:", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"] +
+            epilogue_core(dt) + [f"s_setpc_b64 s[{SRA}:{SRA + 1}]"])
+
+
+def epilogue_core(dt):
+    out = []
     inv, L, t, lse, cls = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}", f"v{MISC + 3}", f"v{MISC + 4}"
     n = 0
     for rb in (0, 1):
