@@ -35,6 +35,12 @@
 
 namespace xfa {
 
+// cache policy of the K/V stream loads (buffer aux bits; A/B builds: -DXFA_DEC_CPOL=2 is the
+// non-temporal hint on gfx950)
+#ifndef XFA_DEC_CPOL
+#define XFA_DEC_CPOL 0
+#endif
+
 constexpr int kDecKeys = 32;        // keys per tile (one 32x32 MFMA block of S^T)
 constexpr int kDecWaves = 4;        // waves (= splits) per workgroup
 
@@ -301,16 +307,16 @@ __global__ void __launch_bounds__(NWV * 64, 2) fmha_decode_kernel(const FwdParam
                 // a base left in VGPRs made every load a (single-trip) waterfall loop
                 const __amdgpu_buffer_rsrc_t krs = make_rsrc(uniform_ptr(kpool + (int64_t)page * p.k_batch * ESZ), page_k);
                 const __amdgpu_buffer_rsrc_t vrs = make_rsrc(uniform_ptr(vpool + (int64_t)page * p.v_batch * ESZ), page_v);
-                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_k, x * krow_b, 0);
-                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_v, x * vrow_b, 0);
+                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_k, x * krow_b, XFA_DEC_CPOL);
+                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_v, x * vrow_b, XFA_DEC_CPOL);
             }
         } else {
             // rows >= sk fall outside the sequence descriptor and read as zeros
 #pragma unroll
             for (int i = 0; i < NLD; ++i) {
                 const int n = t * kDecKeys + RPI * i;
-                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(kseq_rs, lane_k, n * krow_b, 0);
-                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vseq_rs, lane_v, n * vrow_b, 0);
+                kr[i] = __builtin_amdgcn_raw_buffer_load_b128(kseq_rs, lane_k, n * krow_b, XFA_DEC_CPOL);
+                vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vseq_rs, lane_v, n * vrow_b, XFA_DEC_CPOL);
             }
         }
     };
