@@ -114,7 +114,8 @@ void fmha_set_rng_state(uint64_t seed, uint64_t offset);
  * to rng_out[0..1] (device int64 x 2, may be NULL; the reference's params.rng_state).  The
  * backward of that forward: fmha_set_rng_state_device(rng_out, rng_out + 1, 0, NULL).
  * seed_ptr == NULL keeps the host key of fmha_set_rng_state (rng_out still receives it).
- * One-shot: consumed by the next call with p_dropout > 0 (fmha_set_rng_state clears it too). */
+ * One-shot: consumed by the next entry that takes p_dropout, whatever its value or outcome
+ * (fmha_set_rng_state clears it too). */
 void fmha_set_rng_state_device(const int64_t* seed_ptr, const int64_t* offset_ptr,
                                uint64_t offset_add, int64_t* rng_out);
 

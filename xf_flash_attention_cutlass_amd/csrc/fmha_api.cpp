@@ -229,6 +229,14 @@ thread_local const int64_t* g_seed_ptr = nullptr;
 thread_local const int64_t* g_offset_ptr = nullptr;
 thread_local uint64_t g_offset_add = 0;
 thread_local int64_t* g_rng_out = nullptr;
+// The device key is consumed by the next compute entry whatever its outcome (a call that fails
+// validation before set_dropout must not leave a stale rng_out for a later one)
+struct DevRngScope {
+    ~DevRngScope() {
+        g_seed_ptr = g_offset_ptr = nullptr;
+        g_rng_out = nullptr;
+    }
+};
 
 template <typename P>
 bool set_dropout(P& p, float p_dropout, float softcap) {
@@ -245,9 +253,6 @@ bool set_dropout(P& p, float p_dropout, float softcap) {
     p.seed_ptr = g_seed_ptr;
     p.offset_ptr = g_offset_ptr;
     p.rng_out = g_rng_out;
-    // the device key is one-shot: a later call cannot write through a stale rng_out
-    g_seed_ptr = g_offset_ptr = nullptr;
-    g_rng_out = nullptr;
     return true;
 }
 
@@ -415,6 +420,7 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
               const bool return_softmax, bool is_fp16, int num_splits) {
     try {
         clear_error();
+        DevRngScope rng_scope;
         if (!check_common(q_ptr, k_ptr, v_ptr, o_ptr, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
         REQUIRE(!return_softmax || p_dropout > 0.f, "return_softmax is only supported when p_dropout > 0.0");
@@ -448,6 +454,7 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
                       float p_dropout, void* s_dmask) {
     try {
         clear_error();
+        DevRngScope rng_scope;
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(st != nullptr, "strides must be non-null");
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
@@ -545,6 +552,7 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         float p_dropout, void* s_dmask) {
     try {
         clear_error();
+        DevRngScope rng_scope;
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(cu_seqlens_q && (cu_seqlens_k || block_table),
                 "cu_seqlens_q and cu_seqlens_k (or a block table) must be given");
@@ -789,6 +797,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
               hipStream_t stream, void* workspace, size_t workspace_bytes) {
     try {
         clear_error();
+        DevRngScope rng_scope;
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
@@ -848,6 +857,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
                      void* softmax_d, float p_dropout) {
     try {
         clear_error();
+        DevRngScope rng_scope;
         if (!check_common(q, k, v, out, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(head_size <= 256, "the backward supports head dimension at most 256 (got %d)", head_size);
         REQUIRE(dout && softmax_lse && dq && dk && dv, "dout/softmax_lse/dq/dk/dv must be non-null");
