@@ -64,6 +64,7 @@ NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's s
 ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
+QONT = ""             # cache policy suffix of the Q loads and the O / LSE stores (" nt": non-temporal)
 EPI_IDLE = True       # a wave's epilogue runs in its first idle step (causal diagonal; round 4,
                       # same box: C2 causal +2.6 %, bit-identical; no idle steps non-causal)
 FF = True             # fall-through loop layout (masked / idle steps and redo stubs out of line;
@@ -587,7 +588,7 @@ def item_program(dt, uid="%="):
     # Q fragments straight into their AGPRs
     for rb in (0, 1):
         for s in range(8):
-            out.append(f"buffer_load_dwordx4 {qtup(rb, s)}, %[qoff{rb}], %[qsrd], 0 offen offset:{32 * s}")
+            out.append(f"buffer_load_dwordx4 {qtup(rb, s)}, %[qoff{rb}], %[qsrd], 0 offen offset:{32 * s}{QONT}")
     # O accumulators zero (while Q and the first tiles are in flight)
     for i in range(128):
         out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
@@ -778,7 +779,7 @@ def epilogue_core(dt):
                 f"v_sub_f32 {lse}, {lse}, v{NM + rb}",
                 f"v_mul_f32 {lse}, 0x3f317218, {lse}",
                 f"v_cndmask_b32 {lse}, {lse}, {pinf}, vcc",
-                f"buffer_store_dword {lse}, {lo[rb]}, %[lsrd], 0 offen"]
+                f"buffer_store_dword {lse}, {lo[rb]}, %[lsrd], 0 offen{QONT}"]
         for d in range(4):
             for gp in (0, 2):
                 vb = 0 if n % 2 == 0 else 32          # two alternating register sets (S buffer A)
@@ -796,7 +797,7 @@ def epilogue_core(dt):
                         f"v_permlane32_swap_b32 v{w0}, v{w0 + 2}",
                         f"v_permlane32_swap_b32 v{w0 + 1}, v{w0 + 3}",
                         "s_nop 1",
-                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], {oo[rb]}, %[osrd], 0 offen offset:{64 * d + 16 * gp}",
+                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], {oo[rb]}, %[osrd], 0 offen offset:{64 * d + 16 * gp}{QONT}",
                         "s_nop 1"]
     return out
 
@@ -960,6 +961,7 @@ if __name__ == "__main__":
     ap.add_argument("--no-ff", dest="ff", action="store_false", help="the branch-around loop layout")
     ap.add_argument("--no-epi-idle", dest="epi_idle", action="store_false",
                     help="epilogue after the loop only")
+    ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     set_mode(a.ps)
@@ -968,6 +970,7 @@ if __name__ == "__main__":
     DMA2H = a.dma2h
     WARM = a.warm
     FF = a.ff
+    QONT = " nt" if a.qont else ""
     EPI_IDLE = a.epi_idle
     if PS or WARM or not FF:
         EPI_IDLE = False                  # (the idle-step epilogue needs the fall-through layout)
