@@ -603,9 +603,11 @@ if __name__ == "__main__":
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
     ap.add_argument("--no-lead2", dest="lead2", action="store_false",
                     help="DMA two steps ahead only (3 V^T fragments prefetched)")
+    ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     ABL = set(x for x in a.abl.split(",") if x)
+    QK_LEAD = a.qklead
     LEAD2 = a.lead2
     # LEAD2: V_{j+3} overwrites V_{j-1}'s slot in step j's first half, before its mid barrier, so
     # every V^T fragment of a tile must be read in the previous step (none after a barrier)
