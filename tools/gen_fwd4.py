@@ -962,6 +962,7 @@ if __name__ == "__main__":
     ap.add_argument("--no-epi-idle", dest="epi_idle", action="store_false",
                     help="epilogue after the loop only")
     ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
+    ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     set_mode(a.ps)
@@ -970,6 +971,7 @@ if __name__ == "__main__":
     DMA2H = a.dma2h
     WARM = a.warm
     FF = a.ff
+    QK_LEAD = a.qklead
     QONT = " nt" if a.qont else ""
     EPI_IDLE = a.epi_idle
     if PS or WARM or not FF:
