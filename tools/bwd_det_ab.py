@@ -1,5 +1,5 @@
-"""In-process timing of the backward with float-atomic dQ vs deterministic per-key-block dQ
-slices (same inputs, interleaved rounds).  python tools/bwd_det_ab.py [--s 4096] [--noncausal]"""
+"""In-process timing of the backward with float-atomic dQ vs the deterministic mode (bounded
+dQ slices walked in key-block order) (same inputs, interleaved rounds).  python tools/bwd_det_ab.py [--s 4096] [--noncausal]"""
 import argparse
 import os
 import statistics
