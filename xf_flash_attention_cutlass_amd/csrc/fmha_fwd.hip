@@ -28,8 +28,7 @@ typedef _Float16 elem_t;
 
 static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
                                  void (*kern)(const CombineParams),
-                                 void (*row_kern)(const CombineParams) = nullptr,
-                                 void (*wave_kern)(const CombineParams) = nullptr) {
+                                 void (*row_kern)(const CombineParams) = nullptr) {
     CombineParams cp;
     cp.oaccum = p.oaccum;
     cp.lseaccum = p.lseaccum;
@@ -44,10 +43,7 @@ static hipError_t launch_combine(const FwdParams& p, int hd, hipStream_t st,
     const int ext = cp.dec_ns ? p.dec_cap : p.num_splits;
     // few rows (the decode shapes): one workgroup per row, all of its partials in flight at once
     if (row_kern && p.comb_row && ext <= 128 && crow <= 8 * (int64_t)p.num_cus) {
-        if (p.comb_row == 2 && wave_kern)        // one wave per row, every partial in flight
-            hipLaunchKernelGGL(wave_kern, dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
-        else
-            hipLaunchKernelGGL(row_kern, dim3((unsigned)crow), dim3(256), 0, st, cp);
+        hipLaunchKernelGGL(row_kern, dim3((unsigned)crow), dim3(256), 0, st, cp);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)((crow + 3) / 4)), dim3(256), 0, st, cp);
@@ -91,8 +87,7 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     if (e != hipSuccess) return e;
     if (p.dec_ctr) return hipSuccess;          // the last split of each (b, kv head) merged
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>,
-                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr,
-                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_wave_kernel<HD, T> : nullptr);
+                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr);
 }
 
 template <int HD, typename T, int NW>
@@ -130,8 +125,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
     return launch_combine(p, HD, st, fmha_combine_kernel<HD, T>,
-                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr,
-                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_wave_kernel<HD, T> : nullptr);
+                          (HD == 64 || HD == 128 || HD == 256) ? fmha_combine_row_kernel<HD, T> : nullptr);
 }
 
 #if XFA_HD == 128

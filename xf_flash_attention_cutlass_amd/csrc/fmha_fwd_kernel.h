@@ -964,94 +964,4 @@ __global__ void __launch_bounds__(256) fmha_combine_row_kernel(const CombinePara
     }
 }
 
-// Split-KV combine, one wave per row with every partial of the row in flight at once (comb_row
-// 2): lane l owns float4 chunk l % (HD / 4) of the splits s = g, g + G, ... (g = l / (HD / 4),
-// G = 64 / (HD / 4)), loads up to 16 of them plus their LSEs before any use, merges the LSEs
-// across the wave (max, then the sum counted once per split by the chunk-0 lane of each group)
-// and sums the weighted partials of the G groups with permlane swaps: no LDS, no barrier, one
-// memory latency per row for <= 16 G splits.  HD in {64, 128, 256}, at most 128 splits.
-template <int HD, typename T>
-__global__ void __launch_bounds__(256) fmha_combine_wave_kernel(const CombineParams cp) {
-    constexpr int D4 = HD / 4;
-    constexpr int G = 64 / D4;
-    constexpr int NB = 16;
-    static_assert(G * D4 == 64, "chunks per wave");
-    const int lane = threadIdx.x & 63;
-    const int64_t rid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t rows = (int64_t)cp.b * cp.h * cp.seqlen_q;
-    if (rid >= rows) return;
-    const int pos = (int)(rid % cp.seqlen_q);
-    const int head = (int)((rid / cp.seqlen_q) % cp.h);
-    const int bidx = (int)(rid / ((int64_t)cp.seqlen_q * cp.h));
-    const int ns = cp.dec_ns ? cp.dec_ns[bidx] : cp.num_splits;
-    const int c = lane % D4, g = lane / D4;
-    const float* oa = cp.oaccum + rid * HD + 4 * c;
-    const int64_t sstride = rows * HD;
-    f32x4 x[NB];
-    float ls[NB];
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-        const int sp = g + G * u;
-        x[u] = sp < ns ? *reinterpret_cast<const f32x4*>(oa + sp * sstride) : f32x4{0.f, 0.f, 0.f, 0.f};
-        ls[u] = sp < ns ? cp.lseaccum[sp * rows + rid] : -INFINITY;
-    }
-    // splits past the first NB rounds (long ragged sequences): their LSEs only, for the merge
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < NB; ++u) mx = fmaxf(mx, ls[u]);
-    for (int sp = g + G * NB; sp < ns; sp += G) mx = fmaxf(mx, cp.lseaccum[sp * rows + rid]);
-    mx = wave_max_halves(mx);
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-    float sum = 0.f;
-    if (c == 0 && mx != -INFINITY) {
-#pragma unroll
-        for (int u = 0; u < NB; ++u) sum += __expf(ls[u] - mx);
-        for (int sp = g + G * NB; sp < ns; sp += G) sum += __expf(cp.lseaccum[sp * rows + rid] - mx);
-    }
-    sum = wave_sum_halves(sum);
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
-    const bool empty = (mx == -INFINITY) || sum == 0.f;
-    const float lse = empty ? INFINITY : __logf(sum) + mx;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (!empty) {
-#pragma unroll
-        for (int u = 0; u < NB; ++u) acc += __expf(ls[u] - lse) * x[u];
-        for (int s0 = g + G * NB; s0 < ns; s0 += G * NB) {
-#pragma unroll
-            for (int u = 0; u < NB; ++u) {
-                const int sp = s0 + G * u;
-                if (sp < ns) {
-                    x[u] = *reinterpret_cast<const f32x4*>(oa + sp * sstride);
-                    ls[u] = cp.lseaccum[sp * rows + rid];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < NB; ++u)
-                if (s0 + G * u < ns) acc += __expf(ls[u] - lse) * x[u];
-        }
-    }
-    // the G groups of one chunk: lanes c + D4 g
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float v = acc[i];
-        if constexpr (G == 4) {
-            auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-            v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-        }
-        if constexpr (G >= 2) v = wave_sum_halves(v);
-        acc[i] = v;
-    }
-    if (g == 0) {
-        T* orow = reinterpret_cast<T*>(cp.o) + (int64_t)bidx * cp.o_batch + (int64_t)pos * cp.o_row +
-                  (int64_t)head * cp.o_head;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (4 * c + i < cp.d) orow[4 * c + i] = (T)acc[i];
-    }
-    if (cp.lse && lane == 0)
-        cp.lse[(int64_t)bidx * cp.lse_batch + (int64_t)head * cp.lse_head + pos] = lse;
-}
-
 }  // namespace xfa
