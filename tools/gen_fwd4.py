@@ -64,6 +64,7 @@ NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's s
 ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
+DMAFIRST = False      # main steps: the 8 DMA pieces in gaps 0..7, the softmax in gaps 8..63
 QONT = ""             # cache policy suffix of the Q loads and the O / LSE stores (" nt": non-temporal)
 EPI_IDLE = True       # a wave's epilogue runs in its first idle step (causal diagonal; round 4,
                       # same box: C2 causal +2.6 %, bit-identical; no idle steps non-causal)
@@ -298,8 +299,9 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
     sm = []      # (gap, seq, texts)
     if kind & SM and not ("nosm" in ABL and kind & PV):
         span = G if G else 64
+        d0 = 8 if (DMAFIRST and G == 64) else 0      # DMAFIRST: no softmax in the DMA gaps 0..7
         for v in range(64):
-            tg = (v * span) // 64
+            tg = d0 + (v * (span - d0)) // 64
             for stage, txt in sm_value_ops(dt, v, sc_buf, pn_buf, mask, nt):
                 sm.append((tg + stage, 4 * v + stage, txt))
 
@@ -321,6 +323,8 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
     for n, wi in enumerate(dmas):
         if DMA2H:
             g = min(mid + 1 + (n * max(1, G - mid - 4)) // len(dmas), G - 1)
+        elif DMAFIRST and G == 64:
+            g = n
         else:
             g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
@@ -962,6 +966,7 @@ if __name__ == "__main__":
     ap.add_argument("--no-epi-idle", dest="epi_idle", action="store_false",
                     help="epilogue after the loop only")
     ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
+    ap.add_argument("--dmafirst", action="store_true", help="DMA pieces in gaps 0..7, softmax after")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
@@ -973,6 +978,7 @@ if __name__ == "__main__":
     FF = a.ff
     QK_LEAD = a.qklead
     QONT = " nt" if a.qont else ""
+    DMAFIRST = a.dmafirst
     EPI_IDLE = a.epi_idle
     if PS or WARM or not FF:
         EPI_IDLE = False                  # (the idle-step epilogue needs the fall-through layout)
