@@ -138,6 +138,46 @@ def test_dropout_varlen_vs_oracle(xfa):
         ok += bb
 
 
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_dropout_varlen_fwd_bwd_vs_oracle(xfa, parity_report, deterministic):
+    """Varlen forward + backward with dropout: dq / dk / dv of every sequence
+    against the oracle given the kernel's mask, under the reference's 3x + 1e-5 rule."""
+    torch.manual_seed(5)
+    p, h, hk, d = 0.2, 4, 2, 64
+    lq, lk = [64, 130, 1, 97], [150, 130, 40, 200]
+    cq = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32, device=DEV)
+    ck = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(lq), h, d, dtype=torch.bfloat16)
+    k = torch.randn(sum(lk), hk, d, dtype=torch.bfloat16)
+    v = torch.randn(sum(lk), hk, d, dtype=torch.bfloat16)
+    dout = torch.randn(sum(lq), h, d, dtype=torch.bfloat16)
+    qg, kg, vg = (x.to(DEV).requires_grad_(True) for x in (q, k, v))
+    out, lse, s = xfa.flash_attn_varlen_func(qg, kg, vg, cq, ck, max(lq), max(lk), dropout_p=p,
+                                             causal=True, deterministic=deterministic,
+                                             return_attn_probs=True)
+    dq, dk, dv = (g.float().cpu() for g in torch.autograd.grad(out, (qg, kg, vg), dout.to(DEV)))
+    oq = ok = 0
+    for i, (a, bb) in enumerate(zip(lq, lk)):
+        mask = ~torch.signbit(s[i:i + 1, :, :a, :bb].float()).cpu()
+        grads = []
+        for upcast in (True, False):
+            qq = q[None, oq:oq + a].clone().requires_grad_(True)
+            kk = k[None, ok:ok + bb].clone().requires_grad_(True)
+            vv = v[None, ok:ok + bb].clone().requires_grad_(True)
+            o, _ = orc.attention_ref(qq, kk, vv, None, None, None, p, mask, causal=True,
+                                     upcast=upcast, reorder_ops=not upcast)
+            grads.append(torch.autograd.grad(o, (qq, kk, vv), dout[None, oq:oq + a]))
+        got = (dq[oq:oq + a], dk[ok:ok + bb], dv[ok:ok + bb])
+        for name, g, r, pt in zip(("dq", "dk", "dv"), got, grads[0], grads[1]):
+            e = (g - r[0].float()).abs().max().item()
+            bnd = 3 * (pt[0].float() - r[0].float()).abs().max().item() + 1e-5
+            parity_report({"case": f"dropout varlen seq{i} {a}x{bb} det={deterministic} {name}",
+                           "err": e, "bound": bnd, "ok": e <= bnd})
+            assert e <= bnd, (i, name, e, bnd)
+        oq += a
+        ok += bb
+
+
 def test_dropout_deterministic_bwd_bitwise(xfa):
     torch.manual_seed(4)
     q = torch.randn(2, 300, 4, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
