@@ -65,6 +65,7 @@ ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm no
 DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
 WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
 DMAFIRST = False      # main steps: the 8 DMA pieces in gaps 0..7, the softmax in gaps 8..63
+EVENGAP = False       # G = 64 steps: LDS reads and DMA pieces in even gaps (the odd ones carry the cvts)
 QONT = ""             # cache policy suffix of the Q loads and the O / LSE stores (" nt": non-temporal)
 EPI_IDLE = True       # a wave's epilogue runs in its first idle step (causal diagonal; round 4,
                       # same box: C2 causal +2.6 %, bit-identical; no idle steps non-causal)
@@ -259,12 +260,16 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
             s, kt = f // 2, f % 2
             lo = klast[f - KS] + 2 if f >= KS else 0
             g = min(max(lo, kfirst[f] - READ_LEAD, 0), kfirst[f] - 1)
+            if EVENGAP and G == 64 and g & 1 and g - 1 >= lo:
+                g -= 1
             reads.append((g, 0, f"ds_read_b128 {ktup(f % KS)}, %[kb{s & 1}] offset:{kro + kt * 4 * RB + 512 * (s >> 1)}", ("K", f)))
     if kind & PV:
         for f in range(NVPRE, 16):
             ks, d = f // 4, f % 4
             lo = vlast[f - VS] + 2 if f >= VS else 0
             g = min(max(lo, vfirst[f] - READ_LEAD, 0), vfirst[f] - 1)
+            if EVENGAP and G == 64 and g & 1 and g - 1 >= lo:
+                g -= 1
             off = vro + 2 * ks * RB + 512 * d
             reads.append((g, 1, f"ds_read_b64_tr_b16 {vtup(f % VS, 0)}, %[vb0] offset:{off}", ("V", f)))
             reads.append((g, 2, f"ds_read_b64_tr_b16 {vtup(f % VS, 1)}, %[vb1] offset:{off}", ("V", f)))
@@ -325,6 +330,8 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
             g = min(mid + 1 + (n * max(1, G - mid - 4)) // len(dmas), G - 1)
         elif DMAFIRST and G == 64:
             g = n
+        elif EVENGAP >= 2 and G == 64:
+            g = 2 * (1 + (n * (mid // 2 - 1)) // len(dmas))
         else:
             g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
@@ -967,6 +974,7 @@ if __name__ == "__main__":
                     help="epilogue after the loop only")
     ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
     ap.add_argument("--dmafirst", action="store_true", help="DMA pieces in gaps 0..7, softmax after")
+    ap.add_argument("--evengap", type=int, default=0, help="1: LDS reads, 2: + DMA off the cvt gaps")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
@@ -979,6 +987,7 @@ if __name__ == "__main__":
     QK_LEAD = a.qklead
     QONT = " nt" if a.qont else ""
     DMAFIRST = a.dmafirst
+    EVENGAP = a.evengap
     EPI_IDLE = a.epi_idle
     if PS or WARM or not FF:
         EPI_IDLE = False                  # (the idle-step epilogue needs the fall-through layout)
