@@ -331,7 +331,7 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
         elif DMAFIRST and G == 64:
             g = n
         elif EVENGAP >= 2 and G == 64:
-            g = 2 * (1 + (n * (mid // 2 - 1)) // len(dmas))
+            g = 2 * (1 + (n * (mid // 2 - 1)) // len(dmas)) - (EVENGAP == 3)
         else:
             g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
@@ -974,7 +974,7 @@ if __name__ == "__main__":
                     help="epilogue after the loop only")
     ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
     ap.add_argument("--dmafirst", action="store_true", help="DMA pieces in gaps 0..7, softmax after")
-    ap.add_argument("--evengap", type=int, default=0, help="1: LDS reads, 2: + DMA off the cvt gaps")
+    ap.add_argument("--evengap", type=int, default=0, help="1: LDS reads, 2: + DMA off the cvt gaps, 3: reads even, DMA odd")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
