@@ -92,6 +92,8 @@ def parse(argv=None):
                          "the line")
     ap.add_argument("--prewarm-s", type=float, default=1.0,
                     help="untimed seconds of steps before the warmup (GPU clock ramp)")
+    ap.add_argument("--no-monitor", action="store_true",
+                    help="do not sample the GPU clock / power (tools/gpu_monitor.py)")
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="launcher/aggregation self-test on CPU (gloo, a tiny matmul step): "
                          "NOT a benchmark; used by tests/test_bench_launcher.py")
@@ -438,8 +440,9 @@ def measured_traffic(mode):
 
 
 def event_ms(step, steps, stream):
-    """Median per-step time from HIP events recorded on the launch stream around every step
-    (a separate pass: the event records do not sit in the wall-clock timed region)."""
+    """Per-step times from HIP events recorded on the launch stream around every step (a
+    separate pass: the event records do not sit in the wall-clock timed region): (median, min,
+    max) in ms."""
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(steps)]
     for i in range(steps):
@@ -448,7 +451,72 @@ def event_ms(step, steps, stream):
         evs[i][1].record(stream)
     torch.cuda.synchronize()
     ts = sorted(s.elapsed_time(e) for s, e in evs)
-    return ts[len(ts) // 2]
+    return ts[len(ts) // 2], ts[0], ts[-1]
+
+
+class ClockMonitor:
+    """tools/gpu_monitor.py as a child process started BEFORE this process touches the GPU (it
+    samples `amd-smi metric` clocks and socket power about every 0.1 s; nothing is exec'd from a
+    process that has initialised the GPU).  stats(t0, t1) summarises the samples in a window."""
+
+    def __init__(self):
+        import tempfile
+        self.path = os.path.join(tempfile.mkdtemp(prefix="xfa_mon_"), "samples.jsonl")
+        self.proc = None
+        try:
+            self.proc = subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "tools", "gpu_monitor.py"), self.path],
+                stdin=subprocess.PIPE, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except OSError:
+            self.proc = None
+
+    def samples(self):
+        try:
+            with open(self.path) as f:
+                return [json.loads(x) for x in f if x.strip()]
+        except (OSError, ValueError):
+            return []
+
+    def stats(self, t0, t1):
+        ss = [x for x in self.samples() if t0 <= x["t"] <= t1 and x.get("gfx_mhz")]
+        if not ss:
+            return {"samples": 0, "source": "amd-smi metric (no samples in the window)"}
+        per = sorted(sum(x["gfx_mhz"]) / len(x["gfx_mhz"]) for x in ss)   # mean over XCDs
+        pw = sorted(x["power_w"] for x in ss if isinstance(x.get("power_w"), (int, float)))
+        med = lambda v: v[len(v) // 2] if v else None   # noqa: E731
+        return {"samples": len(ss), "window_s": round(t1 - t0, 3),
+                "gfx_mhz_median": round(med(per), 1), "gfx_mhz_min": round(per[0], 1),
+                "gfx_mhz_max": round(per[-1], 1),
+                "power_w_median": med(pw), "power_w_max": pw[-1] if pw else None,
+                "source": "amd-smi metric -c -p (current gfx clock, mean over XCDs; socket power)"}
+
+    def close(self):
+        if self.proc:
+            try:
+                self.proc.stdin.close()
+                self.proc.wait(timeout=5)
+            except (OSError, subprocess.SubprocessError):
+                self.proc.kill()
+            self.proc = None
+
+
+MONITOR = None
+
+
+def clock_stats(t0, t1):
+    return MONITOR.stats(t0, t1) if MONITOR else None
+
+
+def device_info(dev):
+    pr = torch.cuda.get_device_properties(dev)
+    return {"name": pr.name, "arch": pr.gcnArchName, "cus": pr.multi_processor_count,
+            "pci_bus": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+            "hbm_gib": round(pr.total_memory / 2 ** 30, 1)}
+
+
+def last_kernel():
+    from xf_flash_attention_cutlass_amd import capi
+    return capi.lib().fmha_last_kernel().decode() or None
 
 
 def prewarm(step, seconds, sync):
@@ -461,7 +529,8 @@ def prewarm(step, seconds, sync):
         sync()
 
 
-def roofline(w, ms, mode):
+def roofline(w, ev, mode):
+    ms, ms_min, ms_max = ev
     hbm = w["bound"] == "hbm"
     scale_u = 1e9 if hbm else 1e12
     achieved = w["units"] / (ms / 1e3) / scale_u
@@ -470,7 +539,8 @@ def roofline(w, ms, mode):
     roof = {"bound": "mfma" if w["bound"] == "mfma8" else w["bound"], "achieved": round(achieved, 2), "peak": peak,
             "unit": "GB/s" if hbm else "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": tr["bytes"] if tr else None,
-            "algorithmic_per_launch": w["units"], "kernel_ms": round(ms, 4)}
+            "algorithmic_per_launch": w["units"], "kernel_ms": round(ms, 4),
+            "kernel_ms_min": round(ms_min, 4), "kernel_ms_max": round(ms_max, 4)}
     if tr:
         roof["traffic_source"] = tr["file"]
     return roof
@@ -482,6 +552,7 @@ def sub_result(a, mode, dev, stream, **over):
     a = argparse.Namespace(**{**vars(a), **over})
     w = build_workload(a, mode, dev, 0, 1)
     step = w["step"]
+    t_pw = time.time()
     prewarm(step, 0.5, torch.cuda.synchronize)
     for _ in range(a.warmup):
         step()
@@ -493,12 +564,15 @@ def sub_result(a, mode, dev, stream, **over):
     torch.cuda.synchronize()
     wall_ms = (time.perf_counter() - t0) / k * 1e3
     ev = event_ms(step, k, stream)
+    t_end = time.time()
     hbm = w["bound"] == "hbm"
     u = 1e9 if hbm else 1e12
     out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
            "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
            "unit": "GB/s" if hbm else "TFLOP/s",
-           "roofline": roofline(w, ev, mode + ("_ragged" if a.ragged else ""))}
+           "roofline": roofline(w, ev, mode + ("_ragged" if a.ragged else "")),
+           "kernel": last_kernel(),
+           "gpu_clock": clock_stats(t_pw + 0.2, t_end)}
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = w["cpu"]()
     del w
@@ -573,6 +647,21 @@ def main(argv=None):
     if a.selftest_cpu:
         return selftest_cpu(a, rank, world)
 
+    global MONITOR
+    # under a profiler (rocprofv3's preloaded library initialises the GPU before this program
+    # starts) no child process is started at all
+    profiled = any(k.startswith("ROCPROF") for k in os.environ) or \
+        "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if world == 1 and not a.no_monitor and not profiled:
+        MONITOR = ClockMonitor()         # before this process touches the GPU
+    try:
+        return run(a, world, rank, local)
+    finally:
+        if MONITOR:
+            MONITOR.close()
+
+
+def run(a, world, rank, local):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -598,6 +687,7 @@ def main(argv=None):
             step()
         torch.cuda.synchronize()
         step = graph.replay
+    t_pw = time.time()
     prewarm(step, a.prewarm_s, torch.cuda.synchronize)
     for _ in range(a.warmup):
         step()
@@ -616,6 +706,8 @@ def main(argv=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ev_ms = event_ms(step, a.steps, stream)
+    t_end = time.time()
+    kern = last_kernel()
 
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     units = torch.tensor([w["units"]], device=dev, dtype=torch.float64)
@@ -688,6 +780,9 @@ def main(argv=None):
             "library": capi.lib().fmha_version().decode(),
             "config": w["config"],
             "roofline": roofline(w, ev_ms, a.mode + ("_ragged" if a.ragged else "")),
+            "kernel": kern,
+            "device": device_info(dev),
+            "gpu_clock": clock_stats(t_pw + 0.2, t_end),
         }
         if dist:
             line["rccl"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}

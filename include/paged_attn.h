@@ -101,6 +101,13 @@ int fmha_last_status(void);
  * kernel: one split per wave).  Diagnostic, for tests and tuning. */
 int fmha_last_num_splits(void);
 
+/* The forward kernel the last forward call on this thread launched, with its schedule, e.g.
+ * "fmha_fwd4_kernel persistent=2 xcdq=0 grid=256x1x1 block=256" ("" if the call launched no
+ * forward kernel).  persistent: 0 one workgroup per item, 1 boustrophedon, 2 XCD-grouped item
+ * pairs, 3 dynamic queue (xcdq=1: one queue per XCD).  Diagnostic (ABI 2.3), for tests and the
+ * bench line; the combine launch of a split forward is not named. */
+const char* fmha_last_kernel(void);
+
 /* Dropout RNG state of the calling thread: the following forward / backward calls with
  * p_dropout > 0 draw their keep bits from Philox4x32-7 keyed by (seed, offset) over the score
  * coordinates (batch x head, query position, key) - a forward and the backward of the same

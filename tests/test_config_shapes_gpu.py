@@ -56,6 +56,8 @@ def test_c2_full_shape(xfa, parity_report):
     out, lse, _ = xfa.flash_attn_func(q, k, v, causal=True, return_attn_probs=True)
     torch.cuda.synchronize()
     assert _lib().fmha_last_num_splits() == 1
+    kern = _lib().fmha_last_kernel().decode()
+    assert kern.startswith("fmha_fwd4_kernel" if _lib().fmha_get_option(b"fwd_w4") else "fmha_fwd_kernel"), kern
     for b, h in SAMPLE_BH:
         qs, ks, vs = (x[b:b + 1, :, h:h + 1].cpu() for x in (q, k, v))
         ref, _ = orc.attention_ref(qs, ks, vs, causal=True)
@@ -74,6 +76,15 @@ def test_c2_full_shape(xfa, parity_report):
     finally:
         L.fmha_set_option(b"fwd_persistent", 1)
     assert torch.equal(out, out_np)
+    # ... == the per-XCD dynamic item queues (fwd_dyn = 2), twice (self-resetting counters)
+    dyn = L.fmha_get_option(b"fwd_dyn")
+    assert L.fmha_set_option(b"fwd_dyn", 2) == 0
+    try:
+        for _ in range(2):
+            out_dyn = xfa.flash_attn_func(q, k, v, causal=True)
+            assert torch.equal(out, out_dyn)
+    finally:
+        L.fmha_set_option(b"fwd_dyn", dyn)
 
 
 def test_c3_full_shape(xfa, parity_report):

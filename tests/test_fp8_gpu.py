@@ -38,6 +38,8 @@ def _check(xfa, b, h, hk, sq, sk, causal=False, window=(-1, -1), seed=0, out_dty
                                        causal=causal, window_size=window, out_dtype=out_dtype,
                                        return_lse=True)
     torch.cuda.synchronize()
+    if window[0] < 0 or window[0] >= sk:
+        _assert_fp8_w4()
     qd, kd, vd = q8.float() * qs, k8.float() * ks, v8.float() * vs
     w = (window[0], sk) if window[0] >= 0 and window[1] < 0 else window
     ref, _ = orc.attention_ref(qd, kd, vd, causal=causal, window_size=w)
@@ -54,6 +56,16 @@ def _check(xfa, b, h, hk, sq, sk, causal=False, window=(-1, -1), seed=0, out_dty
     assert torch.equal(torch.isinf(lse.cpu()), ~fin)
     assert (lse.cpu()[fin] - lref[fin]).abs().max().item() < 1e-3
     return out
+
+
+def _assert_fp8_w4():
+    """launches without a left window run the 4-wave fp8 kernel (fp8_w4 = 1, the default; the
+    8-wave one under XFA_TEST_OPTIONS=fp8_w4=0)"""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    kern = L.fmha_last_kernel().decode()
+    want = "fmha_fwd8w_kernel" if L.fmha_get_option(b"fp8_w4") else "fmha_fwd_fp8_kernel"
+    assert kern.startswith(want), kern
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -106,6 +118,7 @@ def test_fp8_fwd_c2_shape(xfa, parity_report):
     q8s = [orc.quantize_fp8(t) for t in x]
     (q8, qs), (k8, ks), (v8, vs) = q8s
     out = xfa.flash_attn_fp8_func(q8, k8, v8, qs, ks, vs, causal=True)
+    _assert_fp8_w4()
     for bb, hh in ((0, 0), (3, 31)):
         sl = [t[bb:bb + 1, :, hh:hh + 1].cpu() for t in (q8, k8, v8)]
         ref, _ = orc.attention_ref(*(t.float() * s for t, s in zip(sl, (qs, ks, vs))), causal=True)
@@ -120,3 +133,13 @@ def test_fp8_fwd_c2_shape(xfa, parity_report):
     finally:
         L.fmha_set_option(b"fwd_persistent", 1)
     assert torch.equal(out, out_np)
+    # the per-XCD dynamic item queues (fwd_dyn = 2), twice (the counters reset themselves)
+    dyn = L.fmha_get_option(b"fwd_dyn")
+    assert L.fmha_set_option(b"fwd_dyn", 2) == 0
+    try:
+        for _ in range(2):
+            out_dyn = xfa.flash_attn_fp8_func(q8, k8, v8, qs, ks, vs, causal=True)
+            assert "persistent=3" in L.fmha_last_kernel().decode() or not L.fmha_get_option(b"fp8_w4")
+            assert torch.equal(out, out_dyn)
+    finally:
+        L.fmha_set_option(b"fwd_dyn", dyn)

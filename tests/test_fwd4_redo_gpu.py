@@ -65,7 +65,17 @@ def _fwd(q, k, v, causal, window=(-1, -1)):
     capi.check()
     torch.cuda.synchronize()
     assert _lib().fmha_last_num_splits() == 1
+    _assert_fwd4()
     return o.cpu(), lse.cpu()
+
+
+def _assert_fwd4():
+    """the redo asm runs only in the 4-wave kernel: prove it ran (unless the suite runs under
+    XFA_TEST_OPTIONS=fwd_w4=0, where the 8-wave kernel is the one asked for)"""
+    L = _lib()
+    kern = L.fmha_last_kernel().decode()
+    want = "fmha_fwd4_kernel" if L.fmha_get_option(b"fwd_w4") else "fmha_fwd_kernel"
+    assert kern.startswith(want), kern
 
 
 def _check(o, lse, q, k, v, causal, what, rtol_lse=0.0, o_atol=None):
@@ -179,6 +189,7 @@ def test_fwd4_slack0_varlen(xfa, dtype, causal):
         out, lse, _ = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV),
                                                  cu.to(DEV), max(lens), max(lens), causal=causal,
                                                  return_attn_probs=True)
+        _assert_fwd4()
     torch.cuda.synchronize()
     out, lse = out.cpu(), lse.cpu()
     for i in range(len(lens)):
@@ -232,6 +243,7 @@ def test_fwd4_growing_scores_varlen(xfa):
     out, lse, _ = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV),
                                              cu.to(DEV), max(lens), max(lens), causal=True,
                                              return_attn_probs=True)
+    _assert_fwd4()
     torch.cuda.synchronize()
     out, lse = out.cpu(), lse.cpu()
     for i in range(len(lens)):

@@ -59,25 +59,45 @@ def test_varlen_bwd_slab_guard_dq_accum():
     assert st != 0 and "dq_accum" in msg
 
 
-def test_deterministic_bwd_workspace_independent_of_seqlen_k():
-    """deterministic=True: S = ceil(CUs / (b * hk)) dQ slices (export.cpp:1090-1091's bound), not
-    one per key block, so the workspace does not grow with seqlen_k (no device here: the library
-    assumes MI355X's 256 CUs)."""
+def _acc(tok, h):
+    return -(-(tok * h * 128 * 4) // 256) * 256         # fp32 [tokens][h][128], 256-B rounded
+
+
+def _dsum(tok, h):
+    return -(-(tok * h * 4) // 256) * 256
+
+
+def _cus(L):
+    """The CU count the library sizes for (the live device's, 256 without one): the slice count
+    of b * hk = 1 over a key range longer than CUs x 256 keys."""
+    ws = L.fmha_bwd_workspace_size(256, 1 << 20, 1, 1, 1, 128, True)
+    return (ws - _dsum(256, 1)) // _acc(256, 1)
+
+
+def test_deterministic_bwd_workspace_bounded():
+    """deterministic=True: S = min(ceil(CUs / (b * hk)), key blocks) dQ slices (export.cpp:1090-1091's
+    bound; no workgroup walks more slices than there are 256-key blocks), capped at 8 GiB of
+    slices beyond the first, so the workspace stops growing with seqlen_k."""
     L = capi.lib()
-    acc = lambda tok, h: tok * h * 128 * 4               # noqa: E731  fp32 [tokens][h][128]
-    for b, h, hk, sq in ((4, 32, 32, 16384), (1, 16, 16, 45056), (8, 32, 8, 1024), (1, 1, 1, 4096)):
-        sizes = {sk: L.fmha_bwd_workspace_size(sq, sk, b, h, hk, 128, True)
-                 for sk in (128, 4096, 65536, 1 << 20)}
-        assert len(set(sizes.values())) == 1, sizes
-        slices = -(-256 // (b * hk))
-        dsum = -(-(b * sq * h * 4) // 256) * 256
-        assert sizes[128] == slices * acc(b * sq, h) + dsum
-        assert L.fmha_bwd_workspace_size(sq, 4096, b, h, hk, 128, False) == acc(b * sq, h) + dsum
-        v = {mk: L.fmha_varlen_bwd_workspace_size(b * sq, mk, b, h, hk, 128, True)
-             for mk in (64, 8192, 1 << 19)}
-        assert len(set(v.values())) == 1 and v[64] == sizes[128]
-    # B4 H32 S16384 D128: two slices (the old per-key-block scheme needed 64)
-    assert L.fmha_bwd_workspace_size(16384, 16384, 4, 32, 32, 128, True) < 3 * acc(4 * 16384, 32)
+    cus = _cus(L)
+    assert cus >= 1
+    for b, h, hk, sq in ((4, 32, 32, 16384), (1, 16, 16, 45056), (8, 32, 8, 1024), (1, 1, 1, 4096),
+                         (1, 64, 1, 2048), (2, 32, 4, 4096)):
+        tok = b * sq
+        for sk in (128, 4096, 65536, 1 << 20):
+            nkb = -(-sk // 256)
+            slices = min(-(-cus // (b * hk)), nkb, 1 + (8 << 30) // _acc(tok, h))
+            want = slices * _acc(tok, h) + _dsum(tok, h)
+            assert L.fmha_bwd_workspace_size(sq, sk, b, h, hk, 128, True) == want, (b, h, hk, sq, sk)
+            assert L.fmha_varlen_bwd_workspace_size(tok, sk, b, h, hk, 128, True) == want
+        assert L.fmha_bwd_workspace_size(sq, 4096, b, h, hk, 128, False) == _acc(tok, h) + _dsum(tok, h)
+    # MQA, one sequence of 32k tokens x 64 query heads (1 GiB per slice): the byte cap bounds it
+    # (the CU bound alone asked for 256 slices = 256 GiB)
+    ws = L.fmha_bwd_workspace_size(32768, 32768, 1, 64, 1, 128, True)
+    assert ws <= 9 * _acc(32768, 64) + _dsum(32768, 64)
+    # B4 H32 S16384 D128: at most two slices on a 256-CU device
+    assert L.fmha_bwd_workspace_size(16384, 16384, 4, 32, 32, 128, True) <= (
+        max(2, -(-cus // 128)) * _acc(4 * 16384, 32) + _dsum(4 * 16384, 32))
 
 
 @pytest.mark.parametrize("kw", [dict(dropout_p=0.1), dict(softcap=30.0),

@@ -60,47 +60,40 @@ KS, VS = 8, 4         # K / V^T fragment ring slots (AGPRs a[192:192+4KS], a[256
 NPRE, NVPRE = 4, 0    # K / V^T fragments of the next step read in this step's second half
 # (round 4, same-box A/B: the 8-slot K ring read 8 gaps ahead with 4 fragments prefetched
 #  across the step boundary +2..4 % over 4 slots / 5 gaps / 2; deeper V^T reads and the DMA
-#  issued after the barrier (DMA2H) did not add to it)
-ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo
-DMA2H = False         # step j issues K_{j+5}, V_{j+3} after its barrier (half a step more lead)
-WARM = False          # warm start: an item's tail issues the next item's K_0, K_1 (persistent grids)
-DMAFIRST = False      # main steps: the 8 DMA pieces in gaps 0..7, the softmax in gaps 8..63
-EVENGAP = False       # G = 64 steps: LDS reads and DMA pieces in even gaps (the odd ones carry the cvts)
-QONT = ""             # cache policy suffix of the Q loads and the O / LSE stores (" nt": non-temporal)
+#  issued after the barrier did not add to it)
+ABL = set()           # timing ablations (results INVALID): novm nobar nolgkm nodma nosm noredo mfma16
 EPI_IDLE = True       # a wave's epilogue runs in its first idle step (causal diagonal; round 4,
                       # same box: C2 causal +2.6 %, bit-identical; no idle steps non-causal)
-FF = True             # fall-through loop layout (masked / idle steps and redo stubs out of line;
-                      # round 4, same box: +0.9 % causal, +0.2 % non-causal, bit-identical)
+# The loop layout is fall-through (masked / idle steps and redo stubs out of line; round 4, same
+# box: +0.9 % causal, +0.2 % non-causal, bit-identical).  Options measured and dropped (DESIGN.md
+# 3.1b keeps one line each): DMA after the barrier one tile further ahead (-1 %), the DMA pieces
+# in gaps 0..7 (-2.8 %), even/odd gap placement (noise), warm start (-1.8 % causal), non-temporal
+# Q / O (-4 %), pre-scaled Q (+5 % but LSE 4.9e-3 off, over the 1e-3 gate).
 
-# fixed registers (PS: the pre-scaled body, see set_mode; the map below is the legacy one)
+# fixed registers
 SBASE = (0, 64)       # S buffers A, B
 PBASE = (128, 160)    # P buffers A, B
 TMP = 192             # 8 scratch
 LT, LIM, NM, LRUN = 200, 202, 204, 206
 MISC = 208            # 208..215: 213 = +inf, 214 = -inf
 PINF, NINF = 213, 214
-NMB = None            # PS: v[NMB + 16 rb : +15] = -m of row block rb (the S MFMA chains' C operand)
 NVFIX = 216           # fixed VGPRs v[0:NVFIX-1]
-PS = False
 ABASE_O, ABASE_Q, ABASE_K, ABASE_V = 0, 128, 192, 240
 
 
-def set_mode(ps):
-    """PS (default): Q is scaled by c = softmax_scale * log2(e) once per item (bf16 / fp16
-    rounding of c q, finer than the reference's own q / sqrt(d) rounding in its low-precision
-    oracle) and every QK^T chain starts from C = -m instead of 0, so the MFMA hands the softmax
-    s c - m directly: one v_exp per score, no fma.  Legacy: P = exp2(fma(s, c, -m))."""
-    global PS, TMP, LT, LIM, NM, LRUN, MISC, PINF, NINF, NMB, NVFIX
-    PS = ps
-    if ps:
-        NMB = 192                         # v[192:223]
-        TMP = 224                         # 4 scratch (exp results; the raw S stays for the rare path)
-        LT, LIM, NM, LRUN = 228, 230, 232, 234
-        MISC = PINF = NINF = None         # temps from dead buffers, -inf as a literal
-        NVFIX = 236
-    else:
-        NMB = None
-        TMP, LT, LIM, NM, LRUN, MISC, PINF, NINF, NVFIX = 192, 200, 202, 204, 206, 208, 213, 214, 216
+GUARDS = []   # assembler checks of the return-address signs, emitted after the whole program
+
+
+def addc_ret(reg, ret, pc, back):
+    """high word of a return address s_getpc + (ret - pc): the carry plus the sign extension of
+    the offset (-1 when the return point lies before the stub, 0 after).  An assembler guard,
+    placed at the end of the asm statement (where both labels are defined), fails the build if
+    the layout ever contradicts the sign assumed here (round 4's redo fault: a stub moved after
+    its return point kept the high word 0)."""
+    GUARDS.extend([f".if ({ret} - {pc}) {'>= 0' if back else '< 0'}", ".err", ".endif"])
+    return [f"s_addc_u32 s{reg}, s{reg}, {-1 if back else 0}"]
+
+
 SJ, ST, SKO, SVO, SRA, SCM = 88, 89, 90, 91, 92, 94     # SRA: s[92:93], SCM: s[94:95]
 SKR, SVR = 80, 84     # s[80:83] / s[84:87]: the K / V buffer descriptors of this step's DMA tiles
 
@@ -174,15 +167,9 @@ def sm_value_ops(dt, v, src_buf, dst_buf, mask, nt):
     """the softmax ops of score v: [(stage, [texts])], stage 0 fma, 1 exp(+mask), 2 add, 3 cvt"""
     rb, kt, r, off, dword = value_info(v)
     t = f"v{TMP + v % nt}"
-    if PS:
-        # the score already is s c - m: exp into a scratch (the raw S stays for the rare path)
-        z = 0
-        ex = [f"v_exp_f32 {t}, {se(src_buf, v)}"]
-        ops = []
-    else:
-        z = 1
-        ops = [(0, [f"v_fma_f32 {t}, {se(src_buf, v)}, %[c], v{NM + rb}"])]
-        ex = [f"v_exp_f32 {t}, {t}"]
+    z = 1
+    ops = [(0, [f"v_fma_f32 {t}, {se(src_buf, v)}, %[c], v{NM + rb}"])]
+    ex = [f"v_exp_f32 {t}, {t}"]
     if mask:
         ex += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}", f"v_cndmask_b32 {t}, 0, {t}, vcc"]
     ops.append((z, ex))
@@ -213,18 +200,17 @@ def mfma16_pair(text, dt):
     return "\\n".join(out)
 
 
-def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
-    """instructions of one step at ring phase ph (= j mod 4); use_nm: (PS) the QK^T chains
-    start from C = -m (False only for tile 0, whose m is not known yet)"""
+def step_body(dt, ph, kind, mask, vm=8):
+    """instructions of one step at ring phase ph (= j mod 4)"""
     par = ph & 1
     sn_buf, sc_buf = (0, 1) if par == 0 else (1, 0)      # S_{j+2} -> sn, scores of j+1 in sc
     pc_buf, pn_buf = (0, 1) if par == 0 else (1, 0)      # P_j in pc, P_{j+1} -> pn
     kro = ((ph + 2) & 3) * TILE                          # K_{j+2}
     vro = (ph & 3) * TILE                                # V_j
     kno = ((ph + 3) & 3) * TILE                          # K_{j+3}: the next step's frags 0, 1
-    kdo = ((ph + 1) if DMA2H else ph) % 4 * TILE       # K_{j+4} (DMA; DMA2H: K_{j+5})
+    kdo = ph % 4 * TILE                                  # K_{j+4} (DMA)
     vno = ((ph + 1) & 3) * TILE                          # V_{j+1}: the next step's first V^T frags
-    vdo = VREG + ((ph + 3) if DMA2H else (ph + 2)) % 4 * TILE   # V_{j+2} (DMA2H: V_{j+3})
+    vdo = VREG + (ph + 2) % 4 * TILE                     # V_{j+2} (DMA)
 
     mf = mfma_order(kind)
     G = len(mf)
@@ -238,7 +224,7 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
             s, kt = a, b
             f = 2 * s + kt
             acc = sv(sn_buf, rb * 2 + kt)
-            src = acc if s else (f"v[{NMB + 16 * rb}:{NMB + 16 * rb + 15}]" if PS and use_nm else "0")
+            src = acc if s else "0"
             mfma[g] = f"{mnem} {acc}, {ktup(f % KS)}, {qtup(rb, s)}, {src}"
             if "mfma16" in ABL:
                 mfma[g] = mfma16_pair(mfma[g], dt)
@@ -260,16 +246,12 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
             s, kt = f // 2, f % 2
             lo = klast[f - KS] + 2 if f >= KS else 0
             g = min(max(lo, kfirst[f] - READ_LEAD, 0), kfirst[f] - 1)
-            if EVENGAP and G == 64 and g & 1 and g - 1 >= lo:
-                g -= 1
             reads.append((g, 0, f"ds_read_b128 {ktup(f % KS)}, %[kb{s & 1}] offset:{kro + kt * 4 * RB + 512 * (s >> 1)}", ("K", f)))
     if kind & PV:
         for f in range(NVPRE, 16):
             ks, d = f // 4, f % 4
             lo = vlast[f - VS] + 2 if f >= VS else 0
             g = min(max(lo, vfirst[f] - READ_LEAD, 0), vfirst[f] - 1)
-            if EVENGAP and G == 64 and g & 1 and g - 1 >= lo:
-                g -= 1
             off = vro + 2 * ks * RB + 512 * d
             reads.append((g, 1, f"ds_read_b64_tr_b16 {vtup(f % VS, 0)}, %[vb0] offset:{off}", ("V", f)))
             reads.append((g, 2, f"ds_read_b64_tr_b16 {vtup(f % VS, 1)}, %[vb1] offset:{off}", ("V", f)))
@@ -300,25 +282,21 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
                 f"buffer_load_dwordx4 %[dma{i}], {srd}, 0 offen lds"]
 
     dmas = [] if "nodma" in ABL else [(w, i) for i in range(4) for w in ("K", "V")]
-    nt = 4 if (G in (0, 64) or PS) else 8
+    nt = 4 if G in (0, 64) else 8
     sm = []      # (gap, seq, texts)
     if kind & SM and not ("nosm" in ABL and kind & PV):
         span = G if G else 64
-        d0 = 8 if (DMAFIRST and G == 64) else 0      # DMAFIRST: no softmax in the DMA gaps 0..7
         for v in range(64):
-            tg = d0 + (v * (span - d0)) // 64
+            tg = (v * span) // 64
             for stage, txt in sm_value_ops(dt, v, sc_buf, pn_buf, mask, nt):
                 sm.append((tg + stage, 4 * v + stage, txt))
 
     out = []
     if G == 0:
-        if DMA2H:
-            out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
         for w, i in dmas:
             a, b = dma(w, i)
             out += [a, "s_nop 0", b]
-        if not DMA2H:
-            out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
+        out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
         for _, _, txt in sorted(sm, key=lambda x: (x[0], x[1])):
             out += txt
         out += [r[2] for r in sorted(reads, key=lambda x: (x[0], x[1]))]
@@ -326,14 +304,7 @@ def step_body(dt, ph, kind, mask, use_nm=True, vm=8):
 
     dma_gap = {}
     for n, wi in enumerate(dmas):
-        if DMA2H:
-            g = min(mid + 1 + (n * max(1, G - mid - 4)) // len(dmas), G - 1)
-        elif DMAFIRST and G == 64:
-            g = n
-        elif EVENGAP >= 2 and G == 64:
-            g = 2 * (1 + (n * (mid // 2 - 1)) // len(dmas)) - (EVENGAP == 3)
-        else:
-            g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
+        g = min(1 + (n * max(1, mid - 2)) // len(dmas), mid - 1)
         dma_gap.setdefault(g, []).append(wi)
     # one piece per gap: a gap's M0 writes all precede its loads below
     assert all(len(v) == 1 for v in dma_gap.values()), "two LDS-DMA pieces in one gap"
@@ -399,9 +370,8 @@ def prefetch_order():
 
 
 def step_prep(incr=False):
-    """per step: the buffer descriptors of K_{j+4} and V_{j+2} (DMA2H: K_{j+5}, V_{j+3}; V
-    clamped at tile 0): base advanced to the tile, range = what is left of the workgroup's keys
-    (>= 0).  incr (the main loop, where the previous step's descriptors are one tile behind):
+    """per step: the buffer descriptors of K_{j+4} and V_{j+2} (V clamped at tile 0): base
+    advanced to the tile, range = what is left of the workgroup's keys (>= 0).  incr (the main loop, where the previous step's descriptors are one tile behind):
     advance both by one tile, 8 SALU instead of 15"""
     if incr:
         out = []
@@ -409,7 +379,7 @@ def step_prep(incr=False):
             out += [f"s_add_u32 s{r}, s{r}, %[kstep]", f"s_addc_u32 s{r + 1}, s{r + 1}, 0",
                     f"s_sub_i32 s{r + 2}, s{r + 2}, %[kstep]", f"s_max_i32 s{r + 2}, s{r + 2}, 0"]
         return out
-    kl, vl = (5, 3) if DMA2H else (4, 2)
+    kl, vl = 4, 2
     out = [f"s_add_i32 s{ST}, s{SJ}, {kl}", f"s_mul_i32 s{SKO}, s{ST}, %[kstep]",
            f"s_add_i32 s{ST}, s{SJ}, {vl}", f"s_max_i32 s{ST}, s{ST}, 0",
            f"s_mul_i32 s{SVO}, s{ST}, %[kstep]"]
@@ -468,125 +438,12 @@ def redo_block(dt, par, uid):
     return out
 
 
-def redo_block_ps(dt, par, uid):
-    """PS rare path for the scores in buffer sc (s c - m_old): d = max(0, masked tile max);
-    m += d (NM, the C blocks), O and l scaled by 2^-d, the tile's scores and the next tile's
-    (already in sn, computed against m_old) shifted by -d, the tile's softmax redone.  Temps
-    come from the P buffer of tile j (consumed by this step's PV)."""
-    sc_buf = 1 if par == 0 else 0
-    sn_buf = 1 - sc_buf
-    pn_buf = 1 if par == 0 else 0
-    pc = PBASE[1 - pn_buf]
-    out = [f".Lredo{par}_{uid}:", "s_nop 7", "s_nop 7", "s_nop 3"]
-    mx, t2, dl, alpha, ninf = (f"v{pc + 8 + i}" for i in range(5))
-    out.append(f"v_mov_b32 {ninf}, 0xff800000")
-    for rb in (0, 1):
-        out.append(f"v_mov_b32 {mx}, {ninf}")
-        for vv in range(32):
-            v = rb * 32 + vv
-            _, _, _, off, _ = value_info(v)
-            out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}",
-                    f"v_cndmask_b32 {t2}, {ninf}, {se(sc_buf, v)}, vcc",
-                    f"v_max_f32 {mx}, {mx}, {t2}"]
-        out += [f"v_mov_b32 {t2}, {mx}", "s_nop 1", f"v_permlane32_swap_b32 {mx}, {t2}",
-                "s_nop 1",
-                f"v_max_f32 {mx}, {mx}, {t2}",
-                f"v_max_f32 {dl}, 0, {mx}",                  # d >= 0
-                f"v_exp_f32_e64 {alpha}, -{dl}",
-                f"v_sub_f32 v{NM + rb}, v{NM + rb}, {dl}",
-                "s_nop 0",
-                f"v_mul_f32 v{LRUN + rb}, v{LRUN + rb}, {alpha}"]
-        out += [f"v_mov_b32 v{NMB + 16 * rb + i}, v{NM + rb}" for i in range(16)]
-        for vv in range(32):
-            v = rb * 32 + vv
-            out += [f"v_sub_f32 {se(sc_buf, v)}, {se(sc_buf, v)}, {dl}",
-                    f"v_sub_f32 {se(sn_buf, v)}, {se(sn_buf, v)}, {dl}"]
-        for i in range(64):
-            a = f"a{ABASE_O + 64 * rb + i}"
-            t = f"v{pc + i % 8}"
-            out += [f"v_accvgpr_read_b32 {t}, {a}", f"v_mul_f32 {t}, {t}, {alpha}",
-                    f"v_accvgpr_write_b32 {a}, {t}"]
-        out.append("s_nop 1")
-        # the tile's softmax again, masked, against the new reference
-        ops = []
-        for vv in range(32):
-            v = rb * 32 + vv
-            for stage, txt in sm_value_ops(dt, v, sc_buf, pn_buf, True, 4):
-                ops.append((vv + stage, 4 * vv + stage, txt))
-        for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1])):
-            out += txt
-        out.append("s_nop 0")
-    out += ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
-    return out
-
-
-def redo_check(par, uid, tag):
-    """after a step with SM: any lane's tile sum past the threshold -> rare path; l += tile sums"""
-    if "noredo" in ABL:
-        return [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-    return [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
-            f"v_cmp_lt_f32_e64 s[{SCM}:{SCM + 1}], %[thr], v{LT + 1}",
-            f"s_or_b64 vcc, vcc, s[{SCM}:{SCM + 1}]",
-            "s_nop 1",
-            f"s_cbranch_vccz .Lnr{tag}_{uid}",
-            f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
-            f".Lpc{tag}_{uid}:",
-            f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
-            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, 0",
-            f"s_branch .Lredo{par}_{uid}",
-            f".Lnr{tag}_{uid}:",
-            f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}",
-            f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-
-
 def prologue_dma(dt):
     """the DMA-only prologue steps, after the Q loads: K_0 published at step -3's barrier (and
     Q landed), K_1 / V_0 in flight for the next steps"""
-    if not DMA2H:
-        out = [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
-        out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
-        return out + ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
-    # K_0 -> slot 0, K_1 -> slot 1 through both descriptor sets; then step -3 waits for all
-    # but K_1 (vmcnt 4: Q and K_0), publishes K_0 and issues K_2, V_0 after its barrier
-    out = []
-    for r, t in ((SKR, 0), (SVR, 1)):
-        off = "0" if t == 0 else "%[kstep]"
-        out += [f"s_add_u32 s{r}, %[kblo], {off}", f"s_addc_u32 s{r + 1}, %[kbhi], 0",
-                f"s_sub_i32 s{r + 2}, %[kvbytes], {off}", f"s_max_i32 s{r + 2}, s{r + 2}, 0",
-                f"s_mov_b32 s{r + 3}, 0x20000"]
-    for r, t in ((SKR, 0), (SVR, 1)):
-        for i in range(4):
-            out += [f"s_add_u32 m0, %[kdst], {t * TILE + i * 1024}", "s_nop 0",
-                    f"buffer_load_dwordx4 %[dma{i}], s[{r}:{r + 3}], 0 offen lds"]
-    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False, vm=4)
-    return out
-
-
-def next_k_reads(ph):
-    """the prefetch reads of the first NPRE K fragments of K_{j+3} at phase ph, in prefetch
-    order (what a DMA-only step at phase ph ends with)"""
-    kno = ((ph + 3) & 3) * TILE
-    out = []
-    for f in range(NPRE):
-        s_, kt_ = f // 2, f % 2
-        out.append(f"ds_read_b128 {ktup(f)}, %[kb{s_ & 1}] offset:{kno + kt_ * 4 * RB + 512 * (s_ >> 1)}")
-    return out
-
-
-def warm_issue(uid):
-    """item tail (all waves past their last LDS read): the next item's K_0 -> slot 0, K_1 ->
-    slot 1 by LDS-DMA, so its prologue does not wait for the first tiles' memory latency"""
-    out = [f"s_cmp_eq_u32 %[nxt], 0", f"s_cbranch_scc1 .Lnw_{uid}",
-           f"s_mov_b32 s{SKR}, %[kblo2]", f"s_mov_b32 s{SKR + 1}, %[kbhi2]",
-           f"s_mov_b32 s{SKR + 2}, %[kvb2]", f"s_mov_b32 s{SKR + 3}, 0x20000",
-           f"s_add_u32 s{SVR}, %[kblo2], %[kstep]", f"s_addc_u32 s{SVR + 1}, %[kbhi2], 0",
-           f"s_sub_i32 s{SVR + 2}, %[kvb2], %[kstep]", f"s_max_i32 s{SVR + 2}, s{SVR + 2}, 0",
-           f"s_mov_b32 s{SVR + 3}, 0x20000"]
-    for r, t in ((SKR, 0), (SVR, 1)):
-        for i in range(4):
-            out += [f"s_add_u32 m0, %[kdst], {t * TILE + i * 1024}", "s_nop 0",
-                    f"buffer_load_dwordx4 %[dma{i}], s[{r}:{r + 3}], 0 offen lds"]
-    return out + [f".Lnw_{uid}:"]
+    out = [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
+    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
+    return out + ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
 
 
 def item_program(dt, uid="%="):
@@ -599,19 +456,12 @@ def item_program(dt, uid="%="):
     # Q fragments straight into their AGPRs
     for rb in (0, 1):
         for s in range(8):
-            out.append(f"buffer_load_dwordx4 {qtup(rb, s)}, %[qoff{rb}], %[qsrd], 0 offen offset:{32 * s}{QONT}")
+            out.append(f"buffer_load_dwordx4 {qtup(rb, s)}, %[qoff{rb}], %[qsrd], 0 offen offset:{32 * s}")
     # O accumulators zero (while Q and the first tiles are in flight)
     for i in range(128):
         out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
     # prologue steps j = -4, -3: DMA only (K_0, K_1); j = -2: QK(0); rowmax; j = -1: QK(1)+SM(0)
-    if WARM:
-        # warm item: K_0 / K_1 were issued by the previous item's tail; Q, K_0 and K_1 landed
-        # (vmcnt(0)) and published (barrier), then step -3's reads of K_0
-        out += [f"s_cmp_eq_u32 %[warm], 0", f"s_cbranch_scc1 .Lcold_{uid}",
-                "s_waitcnt vmcnt(0)", "s_barrier"] + next_k_reads(1)
-        out += [f"s_branch .Lwarm_{uid}", f".Lcold_{uid}:"] + prologue_dma(dt) + [f".Lwarm_{uid}:"]
-    else:
-        out += prologue_dma(dt)
+    out += prologue_dma(dt)
     out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(dt, 2, QK, False)
     # reference max of tile 0 (S in buffer A), masked in place
     out += ["s_nop 7", "s_nop 7", "s_nop 3"]
@@ -632,7 +482,7 @@ def item_program(dt, uid="%="):
                 f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
     out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(dt, 3, QK | SM, False)
     out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-    out += main_loop(dt, uid)
+    out += main_loop_ff(dt, uid)
     # rare path bodies
     out += redo_block(dt, 0, uid) + redo_block(dt, 1, uid)
     out += epilogue(dt, uid)
@@ -657,7 +507,7 @@ def redo_check_ff(par, uid, tag):
             f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
             f".Lpc{tag}_{uid}:",
             f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
-            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",
+            *addc_ret(SRA + 1, f".Lnr{tag}_{uid}", f".Lpc{tag}_{uid}", True),
             f"s_branch .Lredo{par}_{uid}"]
     return inline, stub
 
@@ -700,7 +550,7 @@ def main_loop_ff(dt, uid):
                      f".Lpe{ph}_{uid}:",
                      f"s_add_u32 s{SRA}, s{SRA}, .Lnx{ph}_{uid} - .Lpe{ph}_{uid}",
                      # (.Lnx lies before this stub: negative offset, high word + -1 + carry)
-                     f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",
+                     *addc_ret(SRA + 1, f".Lnx{ph}_{uid}", f".Lpe{ph}_{uid}", True),
                      f"s_branch .Lepi_{uid}"]
         else:
             tail.append(f"s_branch .Lnx{ph}_{uid}")
@@ -710,40 +560,10 @@ def main_loop_ff(dt, uid):
     return out + tail
 
 
-def main_loop(dt, uid):
-    if FF:
-        return main_loop_ff(dt, uid)
-    # main loop over steps j = 0 .. ntl-1, unrolled over the 4 ring phases
-    out = [f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
-    for ph in range(4):
-        par = ph & 1
-        out.append(f".Lph{ph}_{uid}:")
-        out += step_prep(incr=True) + lim_dec()
-        out += [f"s_cmp_gt_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Li{ph}_{uid}",
-                f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
-                f"s_cbranch_scc0 .Lm{ph}_{uid}"]
-        out += step_body(dt, ph, QK | SM | PV, False)
-        out += redo_check(par, uid, f"u{ph}")
-        out.append(f"s_branch .Lnx{ph}_{uid}")
-        out.append(f".Lm{ph}_{uid}:")
-        out += step_body(dt, ph, QK | SM | PV, True)
-        out += redo_check(par, uid, f"m{ph}")
-        out.append(f"s_branch .Lnx{ph}_{uid}")
-        out.append(f".Li{ph}_{uid}:")
-        out += step_body(dt, ph, 0, False)
-        out.append(f".Lnx{ph}_{uid}:")
-        out += [f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
-                f"s_cbranch_scc1 .Lexit_{uid}"]
-    out.append(f"s_branch .Lph0_{uid}")
-    return out
-
-
 def epilogue(dt, uid):
     # epilogue: normalise, O rows (16-byte stores after a permlane32 exchange), LSE
     out = [f".Lexit_{uid}:"]
     out += ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
-    if WARM:
-        out += ["s_barrier"] + warm_issue(uid)
     if EPI_IDLE:
         # a wave that went idle before the last step has stored its rows already
         out += [f"s_cmp_eq_u32 s{SKO}, 1", f"s_cbranch_scc1 .Lend_{uid}"]
@@ -765,18 +585,9 @@ def epilogue_idle(dt, uid):
 
 def epilogue_core(dt):
     out = []
-    if PS:
-        # temps and the offsets (from their AGPR operands) in S buffer A above the store sets
-        inv, L, t, lse, cls, pinf = (f"v{56 + i}" for i in range(6))
-        oo, lo = ("v52", "v53"), ("v54", "v55")
-        out += [f"v_mov_b32 {pinf}, 0x7f800000",
-                f"v_accvgpr_read_b32 {oo[0]}, %[ooff0]", f"v_accvgpr_read_b32 {oo[1]}, %[ooff1]",
-                f"v_accvgpr_read_b32 {lo[0]}, %[loff0]", f"v_accvgpr_read_b32 {lo[1]}, %[loff1]",
-                "s_nop 1"]
-    else:
-        inv, L, t, lse = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}", f"v{MISC + 3}"
-        cls, pinf = f"v{MISC + 7}", f"v{PINF}"
-        oo, lo = ("%[ooff0]", "%[ooff1]"), ("%[loff0]", "%[loff1]")
+    inv, L, t, lse = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}", f"v{MISC + 3}"
+    cls, pinf = f"v{MISC + 7}", f"v{PINF}"
+    oo, lo = ("%[ooff0]", "%[ooff1]"), ("%[loff0]", "%[loff1]")
     n = 0
     for rb in (0, 1):
         out += [f"v_mov_b32 {t}, v{LRUN + rb}", "s_nop 1", f"v_permlane32_swap_b32 v{LRUN + rb}, {t}",
@@ -790,7 +601,7 @@ def epilogue_core(dt):
                 f"v_sub_f32 {lse}, {lse}, v{NM + rb}",
                 f"v_mul_f32 {lse}, 0x3f317218, {lse}",
                 f"v_cndmask_b32 {lse}, {lse}, {pinf}, vcc",
-                f"buffer_store_dword {lse}, {lo[rb]}, %[lsrd], 0 offen{QONT}"]
+                f"buffer_store_dword {lse}, {lo[rb]}, %[lsrd], 0 offen"]
         for d in range(4):
             for gp in (0, 2):
                 vb = 0 if n % 2 == 0 else 32          # two alternating register sets (S buffer A)
@@ -808,87 +619,13 @@ def epilogue_core(dt):
                         f"v_permlane32_swap_b32 v{w0}, v{w0 + 2}",
                         f"v_permlane32_swap_b32 v{w0 + 1}, v{w0 + 3}",
                         "s_nop 1",
-                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], {oo[rb]}, %[osrd], 0 offen offset:{64 * d + 16 * gp}{QONT}",
+                        f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], {oo[rb]}, %[osrd], 0 offen offset:{64 * d + 16 * gp}",
                         "s_nop 1"]
     return out
 
 
-def q_prescale(dt):
-    """PS: Q <- dt(c q) in place (fp32 product, one rounding), 16 dwords per batch through the
-    S buffers (free until the first QK^T)"""
-    out = []
-    for b0 in range(0, 64, 16):
-        regs = range(b0, b0 + 16)
-        out += [f"v_accvgpr_read_b32 v{i}, a{ABASE_Q + i}" for i in regs]
-        for i in regs:
-            lo, hi = f"v{64 + i}", f"v{128 + i}"
-            if dt == "bf16":
-                out += [f"v_lshlrev_b32 {lo}, 16, v{i}", f"v_and_b32 {hi}, 0xffff0000, v{i}"]
-            else:
-                out += [f"v_cvt_f32_f16 {lo}, v{i}", f"v_lshrrev_b32 {hi}, 16, v{i}",
-                        f"v_cvt_f32_f16 {hi}, {hi}"]
-        out += [f"v_mul_f32 v{64 + i}, %[c], v{64 + i}" for i in regs]
-        out += [f"v_mul_f32 v{128 + i}, %[c], v{128 + i}" for i in regs]
-        out += [f"v_cvt_pk_{dt}_f32 v{i}, v{64 + i}, v{128 + i}" for i in regs]
-        out += [f"v_accvgpr_write_b32 a{ABASE_Q + i}, v{i}" for i in regs]
-    out.append("s_nop 1")
-    return out
-
-
-def item_program_ps(dt, uid="%="):
-    """PS item: offsets and limits arrive in AGPRs (%[...] "a" operands) and are copied to
-    scratch VGPRs where used; -inf is a literal; temps come from buffers dead at that point"""
-    qv = (62, 63)                        # Q row offsets (S buffer A, before the first QK^T)
-    out = ["s_waitcnt lgkmcnt(0)", "s_nop 1",
-           f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{NM + 1}, 0",
-           f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LRUN + 1}, 0",
-           f"v_accvgpr_read_b32 v{LIM}, %[lim0]", f"v_accvgpr_read_b32 v{LIM + 1}, %[lim1]",
-           f"v_accvgpr_read_b32 v{qv[0]}, %[qoff0]", f"v_accvgpr_read_b32 v{qv[1]}, %[qoff1]",
-           "s_nop 1"]
-    for rb in (0, 1):
-        for st in range(8):
-            out.append(f"buffer_load_dwordx4 {qtup(rb, st)}, v{qv[rb]}, %[qsrd], 0 offen offset:{32 * st}")
-    for i in range(128):
-        out.append(f"v_accvgpr_write_b32 a{ABASE_O + i}, 0")
-    out += [f"s_mov_b32 s{SJ}, -4"] + step_prep() + step_body(dt, 0, 0, False)
-    out += [f"s_mov_b32 s{SJ}, -3"] + step_prep() + step_body(dt, 1, 0, False)
-    out += ["s_waitcnt vmcnt(8)"]        # Q landed (older than j=-3's DMA)
-    out += q_prescale(dt)
-    out += [f"s_mov_b32 s{SJ}, -2"] + step_prep() + step_body(dt, 2, QK, False, use_nm=False)
-    # reference max of tile 0 (S in buffer A, already in log2 units), masked; then m is
-    # subtracted from tile 0 and set as the C operand of every later QK^T chain
-    out += ["s_nop 7", "s_nop 7", "s_nop 3"]
-    mx, t2, ninf = f"v{PBASE[1] + 24}", f"v{PBASE[1] + 25}", f"v{PBASE[1] + 26}"
-    out.append(f"v_mov_b32 {ninf}, 0xff800000")
-    for rb in (0, 1):
-        out.append(f"v_mov_b32 {mx}, {ninf}")
-        for vv in range(32):
-            v = rb * 32 + vv
-            _, _, _, off, _ = value_info(v)
-            out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM + rb}",
-                    f"v_cndmask_b32 {se(0, v)}, {ninf}, {se(0, v)}, vcc",
-                    f"v_max_f32 {mx}, {mx}, {se(0, v)}"]
-        out += [f"v_mov_b32 {t2}, {mx}", "s_nop 1", f"v_permlane32_swap_b32 {mx}, {t2}",
-                "s_nop 1",
-                f"v_max_f32 {mx}, {mx}, {t2}",
-                f"v_sub_f32 {t2}, 0, {mx}",
-                f"v_cmp_lg_f32 vcc, {ninf}, {mx}",
-                f"v_cndmask_b32 v{NM + rb}, 0, {t2}, vcc"]
-        out += [f"v_add_f32 {se(0, rb * 32 + vv)}, {se(0, rb * 32 + vv)}, v{NM + rb}" for vv in range(32)]
-        out += [f"v_mov_b32 v{NMB + 16 * rb + i}, v{NM + rb}" for i in range(16)]
-    out.append("s_nop 4")
-    out += [f"s_mov_b32 s{SJ}, -1"] + step_prep() + step_body(dt, 3, QK | SM, False)
-    out += [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}", f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
-    out += main_loop(dt, uid)
-    out += redo_block_ps(dt, 0, uid) + redo_block_ps(dt, 1, uid)
-    out += epilogue(dt, uid)
-    return out
-
-
 def clobbers():
-    # PS: a[208:239] stay free for the AGPR operands (and the compiler's VGPR spills)
-    agprs = [i for i in range(256) if not (PS and 208 <= i < 240)]
-    regs = [f'"v{i}"' for i in range(NVFIX)] + [f'"a{i}"' for i in agprs]
+    regs = [f'"v{i}"' for i in range(NVFIX)] + [f'"a{i}"' for i in range(256)]
     regs += [f'"s{i}"' for i in range(SKR, SCM + 2)]
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 
@@ -912,29 +649,14 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[loff0] "v"(loff0)', '[loff1] "v"(loff1)']
 
 
-WARM_SIG = ", const int kblo2, const int kbhi2, const int kvb2, const int warm, const int nxt"
-WARM_OPS = ['[kblo2] "s"(kblo2)', '[kbhi2] "s"(kbhi2)', '[kvb2] "s"(kvb2)', '[warm] "s"(warm)',
-            '[nxt] "s"(nxt)']
-
-
-def ops():
-    if WARM:
-        return OPS + WARM_OPS
-    if not PS:
-        return OPS
-    av = ("lim0", "lim1", "qoff0", "qoff1", "ooff0", "ooff1", "loff0", "loff1")
-    return [o.replace('"v"', '"a"') if o.split("]")[0][1:] in av else o for o in OPS]
-
-
 def emit(out=OUT):
     assert 192 + 4 * KS <= 256 - 4 * VS and 16 % KS == 0 and 16 % VS == 0
-    assert NPRE <= KS and NVPRE <= VS and not (PS and (KS > 4 or VS > 4))
+    assert NPRE <= KS and NVPRE <= VS
     lines = [
         "// GENERATED by tools/gen_fwd4.py -- do not edit by hand.",
         "// The 4-wave D = 128 forward's item body (fmha_fwd4_kernel.h): one asm statement with a",
         "// fixed register map; see the generator's docstring for the map and the schedule.",
         "#pragma once",
-        f"#define XFA_FWD4_WARM {1 if WARM else 0}",
         '#include "fmha_common.h"',
         "",
         "namespace xfa {",
@@ -942,13 +664,15 @@ def emit(out=OUT):
         "",
     ]
     for dt in ("bf16", "f16"):
-        prog = item_program_ps(dt) if PS else item_program(dt)
-        lines.append(f"__device__ __forceinline__ void fwd4_item_{dt}({SIG}{WARM_SIG if WARM else ''}) {{")
+        prog = item_program(dt)
+        prog += GUARDS
+        GUARDS.clear()
+        lines.append(f"__device__ __forceinline__ void fwd4_item_{dt}({SIG}) {{")
         lines.append("    asm volatile(")
         for b in prog:
             lines.append(f'        "{b}\\n"')
         lines.append("        :")
-        lines.append("        : " + ",\n          ".join(ops()))
+        lines.append("        : " + ",\n          ".join(OPS))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
         lines.append("")
@@ -960,35 +684,19 @@ def emit(out=OUT):
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ps", action="store_true", help="pre-scaled Q (not the default, DESIGN 3.1b)")
     ap.add_argument("--ks", type=int, default=KS, help="K fragment ring slots")
     ap.add_argument("--vs", type=int, default=VS, help="V^T fragment ring slots")
     ap.add_argument("--lead", type=int, default=READ_LEAD, help="gaps an LDS read leads its MFMA")
     ap.add_argument("--npre", type=int, default=NPRE, help="next-step K frags read early")
     ap.add_argument("--nvpre", type=int, default=NVPRE, help="next-step V^T frags read early")
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
-    ap.add_argument("--dma2h", action="store_true", help="DMA after the barrier, half a step more lead")
-    ap.add_argument("--warm", action="store_true", help="warm start: the next item's K_0, K_1 in the tail")
-    ap.add_argument("--no-ff", dest="ff", action="store_false", help="the branch-around loop layout")
     ap.add_argument("--no-epi-idle", dest="epi_idle", action="store_false",
                     help="epilogue after the loop only")
-    ap.add_argument("--qont", action="store_true", help="non-temporal Q loads and O / LSE stores")
-    ap.add_argument("--dmafirst", action="store_true", help="DMA pieces in gaps 0..7, softmax after")
-    ap.add_argument("--evengap", type=int, default=0, help="1: LDS reads, 2: + DMA off the cvt gaps, 3: reads even, DMA odd")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
-    set_mode(a.ps)
     KS, VS, READ_LEAD, NPRE, NVPRE = a.ks, a.vs, a.lead, a.npre, a.nvpre
     ABL = set(x for x in a.abl.split(",") if x)
-    DMA2H = a.dma2h
-    WARM = a.warm
-    FF = a.ff
     QK_LEAD = a.qklead
-    QONT = " nt" if a.qont else ""
-    DMAFIRST = a.dmafirst
-    EVENGAP = a.evengap
     EPI_IDLE = a.epi_idle
-    if PS or WARM or not FF:
-        EPI_IDLE = False                  # (the idle-step epilogue needs the fall-through layout)
     emit(a.out)

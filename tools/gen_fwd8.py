@@ -70,6 +70,19 @@ QK, SM, PV = 1, 2, 4
 MNEM = "v_mfma_scale_f32_32x32x64_f8f6f4"
 
 
+GUARDS = []   # assembler checks of the return-address signs, emitted after the whole program
+
+
+def addc_ret(reg, ret, pc, back):
+    """high word of a return address s_getpc + (ret - pc): the carry plus the sign extension of
+    the offset (-1 when the return point lies before the stub, 0 after).  An assembler guard,
+    placed at the end of the asm statement (where both labels are defined), fails the build if
+    the layout ever contradicts the sign assumed here (round 4's redo fault: a stub moved after
+    its return point kept the high word 0)."""
+    GUARDS.extend([f".if ({ret} - {pc}) {'>= 0' if back else '< 0'}", ".err", ".endif"])
+    return [f"s_addc_u32 s{reg}, s{reg}, {-1 if back else 0}"]
+
+
 def sv(buf, i):
     b = SBASE[buf] + 16 * i
     return f"v[{b}:{b + 15}]"
@@ -466,7 +479,7 @@ def main_loop(uid, dt):
                  f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
                  f".Lpe{ph}_{uid}:",
                  f"s_add_u32 s{SRA}, s{SRA}, .Lnx{ph}_{uid} - .Lpe{ph}_{uid}",
-                 f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",     # (.Lnx lies before: negative offset)
+                 *addc_ret(SRA + 1, f".Lnx{ph}_{uid}", f".Lpe{ph}_{uid}", True),     # (.Lnx lies before: negative offset)
                  f"s_branch .Lepi_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
     return out + tail + epilogue_idle(uid, dt)
@@ -489,7 +502,7 @@ def redo_check_ff(par, uid, tag):
             f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
             f".Lpc{tag}_{uid}:",
             f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
-            f"s_addc_u32 s{SRA + 1}, s{SRA + 1}, -1",
+            *addc_ret(SRA + 1, f".Lnr{tag}_{uid}", f".Lpc{tag}_{uid}", True),
             f"s_branch .Lredo{par}_{uid}"]
     return inline, stub
 
@@ -584,6 +597,8 @@ def emit(out=OUT):
     ops = [f'[{o}] "s"({o})' for o in SOPS] + [f'[{o}] "v"({o})' for o in VOPS]
     for dt in ("bf16", "f16"):
         prog = item_program(dt)
+        prog += GUARDS
+        GUARDS.clear()
         lines.append(f"__device__ __forceinline__ void fwd8_item_{dt}({SIG}) {{")
         lines.append("    asm volatile(")
         for b in prog:

@@ -1,7 +1,10 @@
 """In-process A/B timing of kernel variants (interleaved rounds, one process, one device —
 cdna_hip_programming.md §5.4 rule 24).
 
-  python tools/perf_ab.py --opt fwd_waves=4,8 [--mode fwd|bwd|fwdbwd] [--rounds 5]
+  python tools/perf_ab.py --opt fwd_waves=4,8 [--mode fwd|bwd|fwdbwd|fwd_fp8] [--rounds 5]
+  python tools/perf_ab.py --var "" --var fwd_dyn=2 --var fwd_persistent=0   (whole variants)
+
+Each variant's line also names the kernel and schedule it ran (fmha_last_kernel).
 """
 from __future__ import annotations
 
@@ -18,7 +21,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--opt", action="append", default=[], help="name=v1,v2,...")
-    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwdbwd"])
+    ap.add_argument("--var", action="append", default=[],
+                    help="one whole variant: name=v,name=v ('' = the defaults); overrides --opt")
+    ap.add_argument("--prewarm", type=float, default=1.0, help="untimed seconds first")
+    ap.add_argument("--mode", default="fwd", choices=["fwd", "bwd", "fwdbwd", "fwd_fp8"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--b", type=int, default=4)
@@ -37,6 +43,10 @@ def main():
     for spec in a.opt:
         name, vals = spec.split("=")
         variants = [v + [(name, int(x))] for v in variants for x in vals.split(",")]
+    if a.var:
+        variants = [[(o.split("=")[0], int(o.split("=")[1])) for o in spec.split(",") if o]
+                    for spec in a.var]
+    defaults = {n: L.fmha_get_option(n.encode()) for vv in variants for n, _ in vv}
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
     hk = a.hk or a.h
     causal = not a.noncausal
@@ -49,7 +59,16 @@ def main():
     sc = a.d ** -0.5
     lse = pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)[5]
 
+    if a.mode == "fwd_fp8":
+        def e4m3(t):                           # per-tensor scale to the e4m3 range (as bench.py)
+            s8 = float(t.float().abs().max()) / 448.0
+            return (t.float() / s8).to(torch.float8_e4m3fn), s8
+        (q8, qs), (k8, ks), (v8, vs) = (e4m3(t) for t in (q, k, v))
+
     def run():
+        if a.mode == "fwd_fp8":
+            pa.fwd_fp8(q8, k8, v8, None, qs, ks, vs, sc, causal, -1, -1, False)
+            return
         if a.mode in ("fwd", "fwdbwd"):
             pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)
         if a.mode in ("bwd", "fwdbwd"):
@@ -57,10 +76,17 @@ def main():
                    False, None, None)
 
     fl = 4.0 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0)
-    fl *= {"fwd": 1.0, "bwd": 2.5, "fwdbwd": 3.5}[a.mode]
+    fl *= {"fwd": 1.0, "bwd": 2.5, "fwdbwd": 3.5, "fwd_fp8": 1.0}[a.mode]
     res = {str(vv): [] for vv in variants}
+    kern = {}
+    import time
+    t = time.perf_counter()
+    while time.perf_counter() - t < a.prewarm:
+        run(); torch.cuda.synchronize()
     for r in range(a.rounds):
         for vv in variants:
+            for name, val in defaults.items():
+                assert L.fmha_set_option(name.encode(), val) == 0
             for name, val in vv:
                 assert L.fmha_set_option(name.encode(), val) == 0, L.fmha_last_error()
             run(); torch.cuda.synchronize()
@@ -70,9 +96,13 @@ def main():
                 run()
             e.record(); torch.cuda.synchronize()
             res[str(vv)].append(s.elapsed_time(e) / a.iters)
+            kern[str(vv)] = L.fmha_last_kernel().decode()
+    for name, val in defaults.items():
+        L.fmha_set_option(name.encode(), val)
     for vv, ts in res.items():
         med = statistics.median(ts)
-        print(f"{a.mode} {vv}: median {med:.4f} ms  min {min(ts):.4f}  -> {fl / med / 1e9:.1f} TFLOP/s")
+        print(f"{a.mode} {vv}: median {med:.4f} ms  min {min(ts):.4f}  max {max(ts):.4f}  -> "
+              f"{fl / med / 1e9:.1f} TFLOP/s  [{kern[vv]}]", flush=True)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,10 @@
 
 Derivations (MI355X_MICROARCH.md):
   * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8;
-    effective clock = cycles / dispatch duration (reads high for dispatches < ~0.3 ms);
+    effective clock = cycles / dispatch duration, reported only for dispatches of >= 50 us
+    (GRBM_GUI_ACTIVE counts the dispatch's ramp and drain beside it: on ~5 us kernels the
+    quotient read 5.5-5.7 GHz in r04); shorter kernels get null, and no utilisation derived
+    from the clock;
   * v_mfma_f32_32x32x16 holds one SIMD's matrix pipe for 32 cycles, 16x16x32 for 16, the
     block-scaled fp8 v_mfma_scale_f32_32x32x64_f8f6f4 for 64 (twice the bf16 form's cycles at 4x
     the K; the fp8 kernels issue only that one): MFMA utilisation = SQ_INSTS_MFMA x 32 (64) / (4 SIMDs x
@@ -30,6 +33,7 @@ import shutil
 import sys
 
 NUM_CUS = 256
+MIN_CLOCK_NS = 50_000      # shortest dispatch whose GRBM cycles / duration is read as a clock
 
 
 def counters(d):
@@ -105,11 +109,12 @@ def main():
             e = {"dispatches_profiled": int(c.get("__dispatches__sq1", 0))}
             cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8
             dur = c.get("__dur_ns__sq1", 0)
+            long_enough = bool(cyc and dur >= MIN_CLOCK_NS)
             if cyc and dur:
                 e["kernel_cycles"] = round(cyc)
                 e["profiled_duration_us"] = round(dur / 1e3, 2)
-                e["effective_clock_ghz"] = round(cyc / dur, 3)
-            if cyc and "SQ_INSTS_MFMA" in c:
+                e["effective_clock_ghz"] = round(cyc / dur, 3) if long_enough else None
+            if long_enough and "SQ_INSTS_MFMA" in c:
                 per = 64 if "fp8" in k or "fwd8" in k else 32
                 e["mfma_util_from_insts"] = round(c["SQ_INSTS_MFMA"] * per / (4 * NUM_CUS * cyc), 4)
             if c.get("SQ_INSTS_MFMA"):

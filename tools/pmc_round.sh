@@ -11,7 +11,7 @@ SQ1="SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY
 SQ2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
 for m in "$@"; do
   case $m in decode_ragged) MA="--mode decode --ragged";; *) MA="--mode $m";; esac
-  B="bench.py $MA --steps 10 --warmup 3 --no-cpu-baseline --no-extras --prewarm-s 0.5"
+  B="bench.py $MA --steps 10 --warmup 3 --no-cpu-baseline --no-extras --no-monitor --prewarm-s 0.5"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/${m}_stats -o run -- python3 $B > gpurun_out/prof/${m}_stats.out 2>&1 || { echo "FAILED stats $m"; exit 1; }
   echo "stats $m"
   for P in sq1 sq2 fetch write; do

@@ -44,13 +44,14 @@ _SIGS = {
     "fmha_last_error": [],
     "fmha_last_status": [],
     "fmha_last_num_splits": [],
+    "fmha_last_kernel": [],
     "fmha_version": [],
     "fmha_set_rng_state": [C.c_uint64, C.c_uint64],
     "fmha_set_rng_state_device": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "fmha_set_option": [C.c_char_p, C.c_int],
     "fmha_get_option": [C.c_char_p],
 }
-_RES = {"fmha_last_error": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
+_RES = {"fmha_last_error": C.c_char_p, "fmha_last_kernel": C.c_char_p, "fmha_version": C.c_char_p, "fmha_last_status": C.c_int,
         "fmha_last_num_splits": C.c_int,
         "fmha_set_option": C.c_int, "fmha_get_option": C.c_int,
         "fmha_bwd_workspace_size_v2": sz, "fmha_varlen_bwd_workspace_size_v2": sz}

@@ -31,6 +31,11 @@ Options& options() {
     static Options o;
     return o;
 }
+thread_local char g_last_kernel[160] = "";   // kernel + schedule of this thread's last forward
+void note_launch(const char* kernel, int persistent, int xcdq, unsigned gx, unsigned gy, unsigned gz, int block) {
+    snprintf(g_last_kernel, sizeof(g_last_kernel), "%s persistent=%d xcdq=%d grid=%ux%ux%u block=%d",
+             kernel, persistent, xcdq, gx, gy, gz, block);
+}
 }  // namespace xfa
 
 namespace {
@@ -304,6 +309,7 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     if (!p.decode) splits = std::max(1, std::min(splits, std::min(128, std::max(1, n_blocks))));
     p.num_splits = splits;
     g_last_splits = splits;
+    g_last_kernel[0] = 0;
     // Ragged caches (per-sequence lengths): the b * splits slots of a kv-head group are shared
     // in proportion to the sequences' key tiles, up to 128 splits for one sequence
     // (fmha_decode_kernel.h dec_slot); equal lengths give the same splits as without.
@@ -348,7 +354,8 @@ extern "C" {
 const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
-const char* fmha_version(void) { return "xf-fmha-gfx950 2.2"; }
+const char* fmha_last_kernel(void) { return g_last_kernel; }
+const char* fmha_version(void) { return "xf-fmha-gfx950 2.3"; }
 
 void fmha_set_rng_state(uint64_t seed, uint64_t offset) {
     g_seed = seed;
@@ -534,7 +541,15 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
         p.max_slack = (float)op.fwd_slack.load();
         p.num_splits = 1;
         p.fwd4 = op.fp8_w4.load();
+        p.xcdq = op.fwd_xcdq.load();
+        // fwd_dyn = 2: the dynamic per-XCD item queues for the dense fp8 launch too
+        p.work_ctr = nullptr;
+        if (op.fwd_dyn.load() == 2) {
+            p.work_ctr = counter_get(stream);
+            REQUIRE(p.work_ctr, "could not allocate the item-queue counters");
+        }
         g_last_splits = 1;
+        g_last_kernel[0] = 0;
         hip_ok(launch_fwd_fp8(p, out_fp16, stream), "fp8 forward launch");
     } catch (...) {
         fail(9, "internal error in fmha_fwd_fp8");
@@ -735,35 +750,51 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
 
 // ------------------------------------------------------------------ backward -----------
 // Workspace: fp32 dq_accum [tokens][h][HD] + fp32 D = rowsum(dO*O) [tokens][h].  Deterministic:
-// S = ceil(CUs / (b * hk)) dq_accum slices (the reference's bound, export.cpp:1090-1091, which
-// counts query heads: here a workgroup covers a kv head's whole GQA group), independent of
-// seqlen_k; workgroup (bh, s) adds key blocks s, s + S, ... into slice s in order.
+// S = min(ceil(CUs / (b * hk)), key blocks) dq_accum slices (the reference's bound,
+// export.cpp:1090-1091, counts query heads: here a workgroup covers a kv head's whole GQA group,
+// and no workgroup walks more slices than there are 256-key blocks), and at most what
+// kDetSliceCap bytes of slices hold; workgroup (bh, s) adds key blocks s, s + S, ... into slice s
+// in order.  Any S >= 1 is a valid schedule (bitwise reproducible for a given S), so a run whose
+// workspace holds fewer slices than its device would pick uses as many as fit.
 static int bwd_block_n_host(int d) { return hd_bucket(d) > 128 ? 128 : 256; }
-static int bwd_slices(int batch, int hk, bool det) {
-    if (!det) return 1;
-    const int units = std::max(1, batch * hk);
-    return std::max(1, (num_cus(current_device()) + units - 1) / units);
-}
 static size_t bwd_acc_bytes(int64_t tokens, int h, int d) {
     return (((size_t)tokens * h * hd_bucket(d) * sizeof(float)) + 255) / 256 * 256;
 }
+static size_t bwd_dsum_bytes(int64_t tokens, int h) {
+    return (((size_t)tokens * h * sizeof(float)) + 255) / 256 * 256;
+}
+constexpr size_t kDetSliceCap = (size_t)8 << 30;     // bytes of dQ slices beyond the first
+static int bwd_slices(int64_t tokens, int batch, int h, int hk, int d, int seqlen_k, bool det) {
+    if (!det) return 1;
+    const int units = std::max(1, batch * hk);
+    const int nkb = std::max(1, (seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d));
+    int s = std::min(nkb, (num_cus(current_device()) + units - 1) / units);
+    const size_t acc = std::max<size_t>(256, bwd_acc_bytes(tokens, h, d));
+    s = (int)std::min<size_t>((size_t)s, 1 + kDetSliceCap / acc);
+    return std::max(1, s);
+}
 static size_t bwd_ws_bytes(int64_t tokens, int h, int d, int slices) {
-    const size_t dsum = (size_t)tokens * h * sizeof(float);
-    return (size_t)slices * bwd_acc_bytes(tokens, h, d) + ((dsum + 255) / 256) * 256;
+    return (size_t)slices * bwd_acc_bytes(tokens, h, d) + bwd_dsum_bytes(tokens, h);
+}
+// slices a caller's workspace of `bytes` holds (0 if not even one)
+static int bwd_slices_fit(int64_t tokens, int h, int d, size_t bytes) {
+    const size_t fixed = bwd_dsum_bytes(tokens, h), acc = std::max<size_t>(1, bwd_acc_bytes(tokens, h, d));
+    return bytes < fixed ? 0 : (int)std::min<size_t>((bytes - fixed) / acc, 1 << 20);
 }
 
-size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t /*seqlen_k*/, int32_t batch_size,
+size_t fmha_bwd_workspace_size(int32_t seqlen_q, int32_t seqlen_k, int32_t batch_size,
                                int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                bool deterministic) {
-    return bwd_ws_bytes((int64_t)batch_size * seqlen_q, num_heads, head_size,
-                        bwd_slices(batch_size, num_heads_k, deterministic));
+    const int64_t tok = (int64_t)batch_size * seqlen_q;
+    return bwd_ws_bytes(tok, num_heads, head_size,
+                        bwd_slices(tok, batch_size, num_heads, num_heads_k, head_size, seqlen_k, deterministic));
 }
 
-size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t /*max_seqlen_k*/, int32_t batch_size,
+size_t fmha_varlen_bwd_workspace_size(int32_t total_q, int32_t max_seqlen_k, int32_t batch_size,
                                       int32_t num_heads, int32_t num_heads_k, int32_t head_size,
                                       bool deterministic) {
     return bwd_ws_bytes(total_q, num_heads, head_size,
-                        bwd_slices(batch_size, num_heads_k, deterministic));
+                        bwd_slices(total_q, batch_size, num_heads, num_heads_k, head_size, max_seqlen_k, deterministic));
 }
 
 // The pre / convert kernels index (token, head, 16-byte chunk) with one 32-bit thread id.
@@ -808,12 +839,16 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
             !slab_ok("k/v/dk/dv", seqlen_k, (int64_t)hk * d, 2) ||
             !slab_ok("dq_accum", seqlen_q, hd_bucket(d), 4) ||
             !bwd_rows_ok((int64_t)batch_size * seqlen_q, h, d)) return;
-        const int slices = bwd_slices(batch_size, hk, deterministic);
-        const size_t need = bwd_ws_bytes((int64_t)batch_size * seqlen_q, h, d, slices);
-        const int nkb = (seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d);
+        const int64_t tok = (int64_t)batch_size * seqlen_q;
+        int slices = bwd_slices(tok, batch_size, h, hk, d, seqlen_k, deterministic);
         char* ws = (char*)workspace;
+        if (ws) {
+            const int fit = bwd_slices_fit(tok, h, d, workspace_bytes);
+            REQUIRE(fit >= 1, "workspace too small (%zu < %zu bytes)", workspace_bytes, bwd_ws_bytes(tok, h, d, 1));
+            slices = std::min(slices, fit);
+        }
+        const size_t need = bwd_ws_bytes(tok, h, d, slices);
         if (!ws) ws = (char*)pool_get(stream, need);
-        else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
         REQUIRE(ws, "could not allocate %zu bytes of backward scratch", need);
         const int hd = hd_bucket(d);
         BwdParams p{};
@@ -822,7 +857,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes((int64_t)batch_size * seqlen_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
-        p.dq_slices = deterministic ? std::min(slices, nkb) : 0;   // slices a workgroup walks into
+        p.dq_slices = deterministic ? slices : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = (int64_t)seqlen_q * h * d;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = p.q_batch;
@@ -870,12 +905,15 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
             !slab_ok("k/v/dk/dv", max_seqlen_k, (int64_t)hk * d, 2) ||
             !slab_ok("dq_accum", max_seqlen_q, hd_bucket(d), 4) ||
             !bwd_rows_ok(total_q, h, d)) return;
-        const int slices = bwd_slices(batch_size, hk, deterministic);
-        const size_t need = bwd_ws_bytes(total_q, h, d, slices);
-        const int nkb = (max_seqlen_k + bwd_block_n_host(d) - 1) / bwd_block_n_host(d);
+        int slices = bwd_slices(total_q, batch_size, h, hk, d, max_seqlen_k, deterministic);
         char* ws = (char*)workspace;
+        if (ws) {
+            const int fit = bwd_slices_fit(total_q, h, d, workspace_bytes);
+            REQUIRE(fit >= 1, "workspace too small (%zu < %zu bytes)", workspace_bytes, bwd_ws_bytes(total_q, h, d, 1));
+            slices = std::min(slices, fit);
+        }
+        const size_t need = bwd_ws_bytes(total_q, h, d, slices);
         if (!ws) ws = (char*)pool_get(stream, need);
-        else REQUIRE(workspace_bytes >= need, "workspace too small (%zu < %zu bytes)", workspace_bytes, need);
         REQUIRE(ws, "could not allocate %zu bytes of backward scratch", need);
         const int hd = hd_bucket(d);
         BwdParams p{};
@@ -884,7 +922,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes(total_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
-        p.dq_slices = deterministic ? std::min(slices, nkb) : 0;   // slices a workgroup walks into
+        p.dq_slices = deterministic ? slices : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
         p.o_row = p.q_row; p.o_head = d; p.o_batch = 0;

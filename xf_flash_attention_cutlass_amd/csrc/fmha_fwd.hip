@@ -65,6 +65,7 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
             (void)hipFuncSetAttribute((const void*)fmha_decode_kernel<HD, T, false, 16, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         });
         const dim3 grid(p.b * p.hk / NWV, p.num_splits);
+        note_launch(p.dec_mr == 16 ? "fmha_decode_kernel<16 rows, 8 heads>" : "fmha_decode_kernel<32 rows, 8 heads>", 0, 0, grid.x, grid.y, grid.z, NWV * 64);
         if (p.dec_mr == 16) {
             if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16, NWV>), grid, dim3(NWV * 64), smem, st, p);
             else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16, NWV>), grid, dim3(NWV * 64), smem, st, p);
@@ -75,6 +76,7 @@ static hipError_t launch_decode(const FwdParams& p, hipStream_t st) {
     } else {
         const size_t smem = (size_t)kDecWaves * 2 * kDecKeys * HD * 2;
         const dim3 grid = p.dec_hmaj ? dim3(p.b * p.hk / kDecWaves, p.num_splits) : dim3(p.b * p.hk, p.num_splits / kDecWaves);
+        note_launch(p.dec_mr == 16 ? "fmha_decode_kernel<16 rows>" : "fmha_decode_kernel<32 rows>", 0, 0, grid.x, grid.y, grid.z, kDecWaves * 64);
         if (p.dec_mr == 16) {
             if (p.kv_fp8) hipLaunchKernelGGL((fmha_decode_kernel<HD, T, true, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
             else hipLaunchKernelGGL((fmha_decode_kernel<HD, T, false, 16>), grid, dim3(kDecWaves * 64), smem, st, p);
@@ -121,6 +123,7 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_kernel<HD, T, NW, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     });
+    note_launch(NW == 8 ? "fmha_fwd_kernel<8 waves>" : "fmha_fwd_kernel<4 waves>", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, NW * 64);
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.num_splits <= 1) return e;
@@ -153,6 +156,7 @@ static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
     constexpr bool BF = std::is_same<elem_t, __bf16>::value;
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd4_kernel<BF>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd4Smem); });
+    note_launch("fmha_fwd4_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 256);
     hipLaunchKernelGGL((fmha_fwd4_kernel<BF>), grid, dim3(256), kFwd4Smem, st, pp);
     return hipGetLastError();
 }

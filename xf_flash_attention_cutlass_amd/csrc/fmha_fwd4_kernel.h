@@ -44,13 +44,9 @@ __device__ __forceinline__ i32x4 fwd4_srd(const void* base, uint32_t bytes) {
     return r;
 }
 
-// One (batch x kv head, 256-row query block) item.  Warm-start bodies (XFA_FWD4_WARM, tools/
-// gen_fwd4.py --warm): `warm` = the previous item's tail already issued this item's K_0 / K_1;
-// bh2 >= 0 names the next item, whose K_0 / K_1 this item's tail issues.  Returns whether the
-// asm body ran (an empty item does not, and then issues nothing for its successor).
+// One (batch x kv head, 256-row query block) item.
 template <bool BF16>
-__device__ __forceinline__ bool fwd4_item(const FwdParams& p, char* smem, const int bh, const int m_block,
-                                          const int warm = 0, const int bh2 = -1) {
+__device__ __forceinline__ void fwd4_item(const FwdParams& p, char* smem, const int bh, const int m_block) {
     constexpr int HD = 128;
     // item-local copies made opaque: otherwise hipcc hoists lane- and parameter-derived values
     // out of the persistent item loop and keeps them live across the asm body
@@ -70,7 +66,7 @@ __device__ __forceinline__ bool fwd4_item(const FwdParams& p, char* smem, const 
     const int G = p.group;
     const int rows_total = sq * G;
     const int row0 = m_block * kFwd4Rows;
-    if (row0 >= rows_total) return false;    // workgroup-uniform
+    if (row0 >= rows_total) return;    // workgroup-uniform
     const int diag = sk - sq;
     auto lim_r = [&](int pos) { return p.wr >= 0 ? min(sk, pos + diag + p.wr + 1) : sk; };
 
@@ -119,7 +115,7 @@ __device__ __forceinline__ bool fwd4_item(const FwdParams& p, char* smem, const 
             for (int c = 0; c < 8; ++c) *reinterpret_cast<u4*>(oseq + ooff[rb] + 32 * c) = u4{0, 0, 0, 0};
             if (p.lse && hh == 0) p.lse[(int64_t)bidx * p.lse_batch + q_off + loff[rb] / 4] = INFINITY;
         }
-        return false;
+        return;
     }
 
     // SRDs: Q / O / LSE of this sequence; K / V of this sequence and kv head, their range ending
@@ -173,46 +169,14 @@ __device__ __forceinline__ bool fwd4_item(const FwdParams& p, char* smem, const 
     (void)kvbytes;
     const int kdst = __builtin_amdgcn_readfirstlane(sbase + wave * 4096);
     const float thr = __builtin_amdgcn_exp2f(p.max_slack);
-#if XFA_FWD4_WARM
-    // the next item's K base and range (its whole sequence: K_0 / K_1 past its own last tile are
-    // masked there like any key past the right edge)
-    int kblo2 = 0, kbhi2 = 0, kvb2 = 0, nxt = 0;
-    if (bh2 >= 0) {
-        const int bidx2 = bh2 / p.hk;
-        const int hk2 = bh2 - bidx2 * p.hk;
-        int k_off2 = 0, sk2 = p.seqlen_k;
-        if (p.cu_seqlens_k) { k_off2 = p.cu_seqlens_k[bidx2]; sk2 = p.cu_seqlens_k[bidx2 + 1] - k_off2; }
-        if (p.seqused_k) sk2 = p.seqused_k[bidx2];
-        if (sk2 > 0) {
-            const char* kseq2 = reinterpret_cast<const char*>(p.k) +
-                                ((int64_t)bidx2 * p.k_batch + (int64_t)k_off2 * p.k_row + (int64_t)hk2 * p.k_head) * 2;
-            kblo2 = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)kseq2);
-            kbhi2 = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)kseq2 >> 32) & 0xFFFF);
-            kvb2 = __builtin_amdgcn_readfirstlane((int)(((sk2 - 1) * k_row + HD) * 2));
-            nxt = 1;
-        }
-    }
-#define XFA_FWD4_WARM_ARGS , kblo2, kbhi2, kvb2, warm, nxt
-#else
-    (void)warm; (void)bh2;
-#define XFA_FWD4_WARM_ARGS
-#endif
     if constexpr (BF16)
         fwd4_item_bf16(kblo, kbhi, vblo, vbhi, (int)kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma[0], dma[0] + 128, dma[1],
-                       dma[1] + 128, lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]
-                       XFA_FWD4_WARM_ARGS);
+                       dma[1] + 128, lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]);
     else
         fwd4_item_f16(kblo, kbhi, vblo, vbhi, (int)kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w,
                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma[0], dma[0] + 128, dma[1],
-                      dma[1] + 128, lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]
-                      XFA_FWD4_WARM_ARGS);
-#undef XFA_FWD4_WARM_ARGS
-#if XFA_FWD4_WARM
-    return nxt != 0;
-#else
-    return false;
-#endif
+                      dma[1] + 128, lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]);
 }
 
 // Persistent grid (one workgroup per CU) walking (b x kv head, row block) items in the
@@ -242,22 +206,13 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd4_kernel(const FwdParams p) {
         m_block = p.n_mblocks - 1 - lin / nbh;
         return 0;
     };
-    int warm = 0;
     for (int k = 0;; ++k) {
         int bh, m_block;
         if (p.persistent == 1 || p.persistent == 2) {
             const int r = static_item(k, bh, m_block);
             if (r == -1) break;
             if (r == -2) continue;
-            // the next item this workgroup runs (warm start)
-            int bh2 = -1, mb2 = 0;
-            for (int k2 = k + 1; k2 <= k + 2; ++k2) {
-                const int r2 = static_item(k2, bh2, mb2);
-                if (r2 == 0) break;
-                bh2 = -1;
-                if (r2 == -1) break;
-            }
-            warm = fwd4_item<BF16>(p, smem, bh, m_block, warm, bh2) ? 1 : 0;
+            fwd4_item<BF16>(p, smem, bh, m_block);
             continue;
         }
         if (p.persistent == 3) {

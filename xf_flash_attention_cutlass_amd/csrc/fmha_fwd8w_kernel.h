@@ -159,16 +159,31 @@ __device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const
                        dv[0], dv[1], lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]);
 }
 
-// Persistent grid (one workgroup per CU): XCD-grouped (n-1-i, i) row-block pairs, as the bf16
-// kernels.
+// Persistent grid (one workgroup per CU): XCD-grouped (n-1-i, i) row-block pairs, or (fwd_dyn
+// = 2) the per-XCD dynamic item queues, as the bf16 kernels.
 template <bool F16>
 __global__ void __launch_bounds__(256, 1) fmha_fwd8w_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int s_claim[2];
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
     for (int k = 0;; ++k) {
         int bh, m_block;
-        if (p.persistent == 2) {
+        if (p.persistent == 3) {
+            const int x = p.xcd_queues ? (int)(blockIdx.x & 7) : 0;
+            const int nq = p.xcd_queues ? (nbh - x + 7) >> 3 : nbh;
+            if (threadIdx.x == 0) s_claim[k & 1] = atomicAdd(p.work_ctr + 2 + x, 1);
+            __syncthreads();
+            const int q = s_claim[k & 1];
+            if (q >= nq * p.n_mblocks) break;
+            if (p.xcd_queues) {
+                bh = x + 8 * (q / p.n_mblocks);
+                m_block = p.n_mblocks - 1 - q % p.n_mblocks;
+            } else {
+                bh = q % nq;
+                m_block = p.n_mblocks - 1 - q / nq;
+            }
+        } else if (p.persistent == 2) {
             const int nm = p.n_mblocks, npair = (nm + 1) >> 1;
             const int bid = (int)blockIdx.x;
             const int v = (bid & 7) * (g >> 3) + (bid >> 3);
@@ -189,6 +204,14 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd8w_kernel(const FwdParams p) {
             m_block = gridDim.y - 1 - blockIdx.y;
         }
         fwd8w_item<F16>(p, smem, bh, m_block);
+    }
+    if (p.persistent == 3 && threadIdx.x == 0) {
+        // the grid's last workgroup resets the queue counters for the next launch on the stream
+        const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+        if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {
+            for (int i = 2; i < 10; ++i) atomicExch(p.work_ctr + i, 0);
+            atomicExch(p.work_ctr + 1, 0);
+        }
     }
 }
 

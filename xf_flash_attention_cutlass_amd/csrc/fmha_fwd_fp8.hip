@@ -17,11 +17,13 @@ static hipError_t launch_fp8_w4(const FwdParams& p, hipStream_t st) {
     dim3 grid(p.b * p.hk, n_mb, 1);
     const int items = p.b * p.hk * n_mb;
     if (p.persist_per_cu > 0 && items > p.num_cus) {
-        pp.persistent = (p.order == 1 && p.num_cus % 8 == 0) ? 2 : 1;
+        pp.persistent = p.work_ctr ? 3 : (p.order == 1 && p.num_cus % 8 == 0) ? 2 : 1;
+        pp.xcd_queues = p.work_ctr && p.xcdq && p.num_cus % 8 == 0 && p.b * p.hk >= 8;
         grid = dim3(p.num_cus, 1, 1);
     }
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8w_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8wSmem); });
+    note_launch("fmha_fwd8w_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 256);
     hipLaunchKernelGGL((fmha_fwd8w_kernel<F16>), grid, dim3(256), kFwd8wSmem, st, pp);
     return hipGetLastError();
 }
@@ -51,6 +53,7 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
         (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         (void)hipFuncSetAttribute((const void*)fmha_fwd_fp8_kernel<T, NW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     });
+    note_launch("fmha_fwd_fp8_kernel<8 waves>", pp.persistent, 0, grid.x, grid.y, grid.z, NW * 64);
     hipLaunchKernelGGL(kern, grid, dim3(NW * 64), smem, st, pp);
     return hipGetLastError();
 }

@@ -49,6 +49,11 @@ struct Options {
 };
 Options& options();
 
+// Records which forward kernel (and schedule) a launch used, for fmha_last_kernel(): the name,
+// the persistent mode (0 = one workgroup per item, 1 boustrophedon, 2 XCD-grouped pairs,
+// 3 dynamic queue), the per-XCD queues flag and the grid.  Thread-local, set by the launchers.
+void note_launch(const char* kernel, int persistent, int xcdq, unsigned gx, unsigned gy, unsigned gz, int block);
+
 // Forward for head dim bucket HD (64 or 128) and dtype; launches the combine when
 // p.num_splits > 1.  Returns the launch status.
 hipError_t launch_fwd_hd64_bf16(const FwdParams& p, hipStream_t st);

@@ -131,6 +131,13 @@ void dropout_rng_restore(float p_dropout, c10::optional<at::Tensor>& rng_state) 
     fmha_set_rng_state((uint64_t)r.data_ptr<int64_t>()[0], (uint64_t)r.data_ptr<int64_t>()[1]);
 }
 
+// Disarms the thread's device dropout key when the binding returns or throws: a check
+// that fails after dropout_rng / dropout_rng_restore, or a forward with seqlen_k == 0 that runs no
+// C entry, must not leave pointers to tensors about to be freed for a later direct C-ABI call.
+struct RngDisarm {
+    ~RngDisarm() { fmha_set_rng_state_device(nullptr, nullptr, 0, nullptr); }
+};
+
 at::Tensor sdmask_buffer(bool want, const at::TensorOptions& opts, int b, int h, int sq, int sk) {
     if (!want) return at::Tensor();
     auto r128 = [](int x) { return (x + 127) / 128 * 128; };
@@ -192,6 +199,7 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
     auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, seqlen_q, seqlen_k);
     auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32, q.device());
+    RngDisarm rng_disarm;
     int64_t alibi_bs = 0;
     at::Tensor alibi = alibi_for_c(alibi_slopes_, batch_size, num_heads, &alibi_bs);
 
@@ -305,6 +313,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     auto softmax_lse = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, max_seqlen_q, max_seqlen_k);
     auto rng_state = dropout_rng(p_dropout, gen_, (int64_t)batch_size * num_heads * 32, q.device());
+    RngDisarm rng_disarm;
     if (zero_tensors) {
         out.zero_();
         softmax_lse.fill_(-std::numeric_limits<float>::infinity());
@@ -537,6 +546,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
     if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     dropout_rng_restore(p_dropout, rng_state);
+    RngDisarm rng_disarm;
     const auto sizes = q.sizes();
     const int batch_size = sizes[0];
     const int seqlen_q = sizes[1];
@@ -607,6 +617,7 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     TORCH_CHECK(p_dropout >= 0.f && p_dropout < 1.f, "p_dropout must be in [0, 1)");
     if (softcap > 0.f) { TORCH_CHECK(p_dropout == 0.f, "Softcapping does not support dropout for now"); }
     dropout_rng_restore(p_dropout, rng_state);
+    RngDisarm rng_disarm;
     TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32, "cu_seqlens_q must have dtype int32");
     TORCH_CHECK(cu_seqlens_k.dtype() == torch::kInt32, "cu_seqlens_k must have dtype int32");
     const int batch_size = cu_seqlens_q.numel() - 1;
