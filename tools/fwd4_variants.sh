@@ -6,6 +6,7 @@
 set -e
 cd "$(dirname "$0")/.."
 python xf_flash_attention_cutlass_amd/build.py --no-ext > /dev/null
+mkdir -p variants
 pids=()
 for spec in "$@"; do
     name="${spec%%=*}"; args="${spec#*=}"
