@@ -665,7 +665,9 @@ def run(a, world, rank, local):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world > 1 or "WORLD_SIZE" in os.environ:
+        # (a one-rank group too when launched by torch.distributed.run: the sharded path and
+        # its RCCL all-gather then run and are timed exactly as at N > 1)
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     _set_options(a.opt)

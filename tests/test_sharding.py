@@ -102,6 +102,18 @@ def _worker(rank, world, port, kind, q):
                                            alibi_slopes=slopes)
             ref = local(x, k, v, causal=True, alibi_slopes=slopes)
             ok = torch.allclose(out, ref, atol=1e-6) and bs.size == (2 if rank == 0 else 1)
+        elif kind == "batch_pref":
+            # prefer="batch" with a batch the world divides: batch shards although the kv heads
+            # would split (the gather along dim 0 needs no copy)
+            x = torch.randn(4, 24, 8, 16)
+            k = torch.randn(4, 24, 4, 16)
+            v = torch.randn(4, 24, 4, 16)
+
+            def local(qq, kk, vv, causal=False):
+                return orc.attention_ref(qq, kk, vv, causal=causal)[0]
+            out, bs = sh.sharded_attention(x, k, v, local_fn=local, causal=True, prefer="batch")
+            ref = local(x, k, v, causal=True)
+            ok = torch.allclose(out, ref, atol=1e-6) and bs.size == 2
         elif kind == "decode":
             # C5 assembly: batch-sharded paged decode, pages stay in the shared pool
             b, hk, h, d, page, sk = 5, 2, 8, 16, 4, 37
@@ -144,7 +156,8 @@ def _worker(rank, world, port, kind, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["heads", "heads_uneven", "heads_alibi", "batch", "decode", "varlen"])
+@pytest.mark.parametrize("kind", ["heads", "heads_uneven", "heads_alibi", "batch", "batch_pref",
+                                  "decode", "varlen"])
 def test_sharded_world2_gloo(kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -92,10 +92,12 @@ def _slice_alibi(alibi, heads: Shard | None = None, batch: Shard | None = None):
 def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
     """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank.
 
-    Even shards (the usual case: heads or batch divisible by the world size) take one
-    all_gather_into_tensor into a rank-major [world, *local.shape] buffer: for dim 0 that buffer
-    IS the result (no copy), otherwise one strided copy interleaves the ranks' pieces along
-    `dim`.  Uneven shards pad to the largest piece along `dim` and drop the padding afterwards."""
+    Even shards (the usual case: heads or batch divisible by the world size): along dim 0 one
+    all_gather_into_tensor whose rank-major buffer IS the result (no copy); along another dim
+    (head shards) the ranks' pieces are gathered straight into their strided views of the
+    assembled output (RCCL lands them in its staging buffer, which torch then scatters into the
+    views: no intermediate [world, ...] tensor and no reshape copy).  Uneven shards pad to the
+    largest piece along `dim` and drop the padding afterwards."""
     dist, rank, world = _world()
     if world == 1:
         return local
@@ -103,12 +105,14 @@ def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
     nmax = max(sizes)
     if min(sizes) == nmax:
         shape = list(local.shape)
-        gathered = local.new_empty([world * shape[0]] + shape[1:])      # rank-major along dim 0
-        dist.all_gather_into_tensor(gathered, local)
         if dim == 0:
+            gathered = local.new_empty([world * shape[0]] + shape[1:])  # rank-major along dim 0
+            dist.all_gather_into_tensor(gathered, local)
             return gathered
         shape[dim] = world * nmax
-        return gathered.view([world] + list(local.shape)).movedim(0, dim).reshape(shape)
+        out = local.new_empty(shape)
+        dist.all_gather(list(out.split(nmax, dim=dim)), local)
+        return out
     shape = list(local.shape)
     shape[dim] = nmax
     buf = local.new_zeros(shape)
@@ -120,17 +124,18 @@ def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
 
 
 def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
-                      local_fn: Callable | None = None, gather: bool = True, **kw):
+                      local_fn: Callable | None = None, gather: bool = True,
+                      prefer: str = "heads", **kw):
     """Dense attention sharded over ranks: every rank holds the full (replicated) q/k/v views,
     computes its GQA-aligned query-head range with `local_fn` (default: the gfx950 kernels)
-    and, if `gather`, all-gathers the outputs.  With fewer kv heads than ranks the batch is
-    sharded instead.  ALiBi slopes in `kw` are sliced to the rank's heads / batch rows.
-    Returns (out, my shard) where the shard is a query-head range, or a batch range
-    (`Shard` with `.batch = True` semantics: see `attention_shards`)."""
+    and, if `gather`, all-gathers the outputs.  With fewer kv heads than ranks, or with
+    prefer="batch" and a batch the world divides (whose gather along dim 0 needs no copy), the
+    batch is sharded instead.  ALiBi slopes in `kw` are sliced to the rank's heads / batch rows.
+    Returns (out, my shard): a query-head range or a batch range (see `attention_shards`)."""
     dist, rank, world = _world()
     if local_fn is None:
         from . import flash_attn_func as local_fn
-    kind, shards = attention_shards(q.shape[0], q.shape[2], k.shape[2], world)
+    kind, shards = attention_shards(q.shape[0], q.shape[2], k.shape[2], world, prefer)
     alibi = kw.pop("alibi_slopes", None)
     if kind == "heads":
         qs, ks = shards[rank]
@@ -151,9 +156,15 @@ def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
     return all_gather_dim(out_local, [s.size for s in shards], 0), bs
 
 
-def attention_shards(batch: int, num_heads: int, num_heads_k: int, world: int):
-    """("heads", [(q heads, kv heads)] per rank) when every rank gets at least one kv head,
-    else ("batch", [batch range] per rank)."""
+def attention_shards(batch: int, num_heads: int, num_heads_k: int, world: int,
+                     prefer: str = "heads"):
+    """("heads", [(q heads, kv heads)] per rank) when every rank gets at least one kv head
+    (unless prefer="batch" and world divides the batch), else ("batch", [batch range] per
+    rank)."""
+    if prefer not in ("heads", "batch"):
+        raise ValueError(f"prefer must be 'heads' or 'batch' (got {prefer!r})")
+    if prefer == "batch" and batch % world == 0:
+        return "batch", batch_shards(batch, world)
     if num_heads_k >= world:
         return "heads", head_shards(num_heads, num_heads_k, world)
     if batch < world:
