@@ -46,7 +46,14 @@ template <int HD> constexpr size_t bwd_smem_bytes() {
 // dQ partial sums -> the fp32 accumulator (deterministic mode: this workgroup's slice, which no
 // other workgroup touches) by float atomics
 __device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
+#if defined(XFA_BWD_ABL) && XFA_BWD_ABL == 1
+    // timing ablation only (tools/quick_variant.py, results INVALID): no dQ atomics, the value
+    // kept live so the dQ phase is not optimised away
+    asm volatile("" :: "v"(v), "v"(off));
+    (void)r;
+#else
     __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
+#endif
 }
 constexpr int kBwdBlockM = 32;               // query rows per tile
 
