@@ -57,7 +57,8 @@ def test_c2_full_shape(xfa, parity_report):
     torch.cuda.synchronize()
     assert _lib().fmha_last_num_splits() == 1
     kern = _lib().fmha_last_kernel().decode()
-    assert kern.startswith("fmha_fwd4_kernel" if _lib().fmha_get_option(b"fwd_w4") else "fmha_fwd_kernel"), kern
+    want = {0: "fmha_fwd_kernel", 1: "fmha_fwd4_kernel", 2: "fmha_fwdpp_kernel"}
+    assert kern.startswith(want[_lib().fmha_get_option(b"fwd_w4")]), kern
     for b, h in SAMPLE_BH:
         qs, ks, vs = (x[b:b + 1, :, h:h + 1].cpu() for x in (q, k, v))
         ref, _ = orc.attention_ref(qs, ks, vs, causal=True)

@@ -70,12 +70,13 @@ def _fwd(q, k, v, causal, window=(-1, -1)):
 
 
 def _assert_fwd4():
-    """the redo asm runs only in the 4-wave kernel: prove it ran (unless the suite runs under
-    XFA_TEST_OPTIONS=fwd_w4=0, where the 8-wave kernel is the one asked for)"""
+    """the redo asm runs only in the generated D = 128 kernels: prove the one asked for ran
+    (fwd_w4 = 1 the 4-wave kernel, 2 the ping-pong kernel; 0 under XFA_TEST_OPTIONS=fwd_w4=0,
+    the compiler-scheduled 8-wave kernel)"""
     L = _lib()
     kern = L.fmha_last_kernel().decode()
-    want = "fmha_fwd4_kernel" if L.fmha_get_option(b"fwd_w4") else "fmha_fwd_kernel"
-    assert kern.startswith(want), kern
+    want = {0: "fmha_fwd_kernel", 1: "fmha_fwd4_kernel", 2: "fmha_fwdpp_kernel"}
+    assert kern.startswith(want[L.fmha_get_option(b"fwd_w4")]), kern
 
 
 def _check(o, lse, q, k, v, causal, what, rtol_lse=0.0, o_atol=None):

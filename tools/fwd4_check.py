@@ -90,7 +90,8 @@ def main():
     ap.add_argument("--time", action="store_true")
     ap.add_argument("--shapes", default="small")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--modes", default="1", help="fwd_w4 values to test (1 normal, 2 all-masked, 3 no-redo)")
+    ap.add_argument("--modes", default="1", help="fwd_w4 values to test against fwd_w4=0 (1 the 4-wave "
+                                                 "kernel, 2 the 8-wave ping-pong kernel)")
     a = ap.parse_args()
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -133,13 +134,13 @@ def main():
     big = [("dense", 4, 4096, 32, 32, True), ("dense", 4, 4096, 32, 32, False),
            ("dense", 2, 3000, 16, 4, True), ("varlen", 0, 0, 16, 8, True),
            ("varlen", 0, 0, 8, 8, False)]
-    for kind, b, s_, h, hk, causal in ([] if a.no_check else big):
+    for mode, kind, b, s_, h, hk, causal in ([] if a.no_check else [(m, *x) for m in modes for x in big]):
         if kind == "dense":
             q = torch.randn(b, s_, h, 128, device=dev, dtype=torch.bfloat16, generator=g)
             k = torch.randn(b, s_, hk, 128, device=dev, dtype=torch.bfloat16, generator=g)
             v = torch.randn(b, s_, hk, 128, device=dev, dtype=torch.bfloat16, generator=g)
             res = []
-            for w4 in (0, 1):
+            for w4 in (0, mode):
                 opt("fwd_w4", w4)
                 out = torch.empty_like(q)
                 r = pa.fwd(q, k, v, out, None, 0.0, 128 ** -0.5, causal, -1, -1, 0.0, False, None)
@@ -151,14 +152,14 @@ def main():
             q = torch.randn(sum(lq), h, 128, device=dev, dtype=torch.bfloat16, generator=g)
             k = torch.randn(sum(lq), hk, 128, device=dev, dtype=torch.bfloat16, generator=g)
             v = torch.randn(sum(lq), hk, 128, device=dev, dtype=torch.bfloat16, generator=g)
-            res = [run(q, k, v, lq, lq, causal, w4) for w4 in (0, 1)]
+            res = [run(q, k, v, lq, lq, causal, w4) for w4 in (0, mode)]
             res = [(o.float(), l) for o, l in res]
         (o8, l8), (o4, l4) = res
         fin = torch.isfinite(l8)
         do = (o4 - o8).abs().max().item()
         dl = (l4[fin] - l8[fin]).abs().max().item()
         worst = max(worst, do)
-        print(f"big {kind} b{b} s{s_} h{h} hk{hk} causal={causal}: |o4-o8|={do:.3e} |dLSE|={dl:.3e} "
+        print(f"big m{mode} {kind} b{b} s{s_} h{h} hk{hk} causal={causal}: |o4-o8|={do:.3e} |dLSE|={dl:.3e} "
               f"nan4={torch.isnan(o4).any().item()}", flush=True)
     print("WORST", worst, flush=True)
     if worst > 0.05:
@@ -168,7 +169,7 @@ def main():
                    for _ in range(3))
         for causal in (True, False):
             fl = 4 * 4 * 32 * 4096 * 4096 * 128 / (2 if causal else 1)
-            for w4 in (0, 1, 0, 1):
+            for w4 in ([0] + modes) * 2:
                 opt("fwd_w4", w4)
                 out = torch.empty_like(q)
                 f = lambda: pa.fwd(q, k, v, out, None, 0.0, 128 ** -0.5, causal, -1, -1, 0.0, False, None)  # noqa

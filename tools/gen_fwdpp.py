@@ -1,0 +1,471 @@
+"""Generate csrc/fmha_fwdpp_body.h: the hand-scheduled body of the 8-wave "ping-pong" D = 128
+forward (csrc/fmha_fwdpp_kernel.h).
+
+Round 5's structure (probe: tools/gen_pingpong.py): one workgroup = 8 waves x
+32 query rows = the 4-wave kernel's 256-row item, TWO waves per SIMD (waves w and w + 4), each
+with 256 registers.  A wave's work alternates between two phases, each closed by an s_barrier:
+
+  M(j)  the MFMA phase: PV(j) then QK^T(j+1)  (32 x v_mfma_f32_32x32x16, K / V^T fragments
+        read from LDS in the gaps, the next PV's first V^T fragments read at its end)
+  V(j)  the VALU phase: softmax(j+1) (fma, exp, row sum per score, cvt per pair) and the
+        wave's share of the LDS-DMA of tile j+3 (4 pieces of 1 KiB: 8 rows of K and of V)
+
+and group B (waves 4-7) runs one phase behind group A (waves 0-3): on every SIMD one wave
+issues MFMAs while its partner issues VALU / DMA.  K / V tiles live in 4-slot LDS rings (the
+kv_off image of the 4-wave kernel); tile t is published at the barrier that closes global phase
+2t-1 (group A: s_waitcnt vmcnt(4) after its V phase, group B: vmcnt(0) after its M phase).
+Measured (probe, C2 shape non-causal, two boxes): 12-13 % more work per clock than the 4-wave
+kernel, 3-4 % more per second at the 1.4 kW board power cap.
+
+Per wave and step j (the loop is unrolled over the 4 ring phases; slot offsets are immediates):
+  unmasked  j+1 <= t_w, j+1 < e_w : M(j), V(j)
+  masked    j+1 <= t_w, j+1 >= e_w: M(j), V(j) with the key-limit mask in the softmax
+  last      j == t_w              : PV(j) only, then the wave's epilogue (O, LSE stores) in V(j)
+  idle      j > t_w               : DMA and barriers only
+(t_w: the wave's last key tile with a visible key, e_w: its first tile needing the edge mask).
+Softmax without a row max in the loop (the 4-wave kernel's scheme): P = exp2(S c - m) against
+m = the masked max of tile 0; a V phase whose partial row sums pass 2^slack takes the rare path
+(true max, O and l rescaled, softmax redone).
+
+Register map (per lane, 256 = v[0:127] + a[0:127]):
+  a[0:63]    O^T accumulators (4 d tiles x 16)
+  a[64:95]   Q fragments (8 x 4), the B operand of S^T = K Q^T
+  a[96:127]  K fragment ring (8 slots x 4)
+  v[0:31]    S (2 x 16: keys 0-31, 32-63 of the tile for this lane's row)
+  v[32:47]   P (4 x 4 packed pairs), the B operand of O^T += V^T P^T
+  v[48:55]   softmax scratch (epilogue / redo temps)
+  v56 tile row sum, v57 -m, v58 running row sum, v59 key limit, v60-63 redo / first-max temps
+  v[64:95]   V^T fragment ring (8 slots x 4)
+  s[80:87]   DMA descriptors (K, V) of the next tile to load; s88 step, s89 temp, s90 stored,
+  s[92:93]   return address, s[94:95] compare mask
+
+  python tools/gen_fwdpp.py        (writes xf_flash_attention_cutlass_amd/csrc/fmha_fwdpp_body.h)
+"""
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "xf_flash_attention_cutlass_amd", "csrc", "fmha_fwdpp_body.h")
+
+HD = 128
+RB = HD * 16           # one 8-row block of the kv_off image
+TILE = 64 * HD * 2     # one K (or V) tile
+KS, VS = 8, 8          # fragment ring slots
+LEAD = 4               # gaps an LDS read leads its MFMA (round 5 A/B: 4 +0.7 % causal over 6)
+NVPRE = 4              # V^T fragments of the next PV read at the end of an M phase
+SBASE, PBASE, TMP = 0, 32, 48
+LT, NM, LRUN, LIM, MISC = 56, 57, 58, 59, 60
+ABASE_O, ABASE_Q, ABASE_K, VBASE_V = 0, 64, 96, 64
+SKR, SVR = 80, 84
+SJ, ST, SST, SRA, SCM = 88, 89, 90, 92, 94
+ABL = set()            # timing ablations (results INVALID): nosm noredo
+DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax (else all first)
+
+GUARDS = []            # assembler checks of the return-address signs, after the whole program
+
+
+def addc_ret(reg, ret, pc, back):
+    """high word of a return address s_getpc + (ret - pc) (see gen_fwd4.addc_ret)"""
+    GUARDS.extend([f".if ({ret} - {pc}) {'>= 0' if back else '< 0'}", ".err", ".endif"])
+    return [f"s_addc_u32 s{reg}, s{reg}, {-1 if back else 0}"]
+
+
+def otup(d):
+    return f"a[{ABASE_O + 16 * d}:{ABASE_O + 16 * d + 15}]"
+
+
+def qtup(s):
+    return f"a[{ABASE_Q + 4 * s}:{ABASE_Q + 4 * s + 3}]"
+
+
+def ktup(slot):
+    return f"a[{ABASE_K + 4 * slot}:{ABASE_K + 4 * slot + 3}]"
+
+
+def vtup(slot, half=None):
+    b = VBASE_V + 4 * slot
+    return f"v[{b}:{b + 3}]" if half is None else f"v[{b + 2 * half}:{b + 2 * half + 1}]"
+
+
+def sv(kt):
+    return f"v[{SBASE + 16 * kt}:{SBASE + 16 * kt + 15}]"
+
+
+def ptup(ks):
+    return f"v[{PBASE + 4 * ks}:{PBASE + 4 * ks + 3}]"
+
+
+def value_info(v):
+    """score v (kt*16 + r) of this lane: key offset in the tile minus 4*hh, P dword"""
+    kt, r = v // 16, v % 16
+    off = 32 * kt + 8 * (r >> 2) + (r & 3)
+    ks = 2 * kt + (r >> 3)
+    return off, ks * 4 + ((r & 7) >> 1)
+
+
+def k_read(f, slot_tile, dst_slot):
+    s, kt = f // 2, f % 2
+    return f"ds_read_b128 {ktup(dst_slot)}, %[kb{s & 1}] offset:{slot_tile * TILE + kt * 4 * RB + 512 * (s >> 1)}"
+
+
+def v_reads(f, slot_tile, dst_slot):
+    ks, d = f // 4, f % 4
+    off = slot_tile * TILE + 2 * ks * RB + 512 * d          # (the lane base carries the V ring)
+    return [f"ds_read_b64_tr_b16 {vtup(dst_slot, h)}, %[vb{h}] offset:{off}" for h in (0, 1)]
+
+
+def m_phase(dt, j_slot, pv=True, qk=True):
+    """PV(j) then QK^T(j+1) (j_slot = j mod 4); with qk the next PV's first NVPRE V^T fragments
+    (tile j+1) are read at the end.  On entry with pv, this tile's first NVPRE V^T fragments are
+    the only LDS reads in flight (the previous M phase's prefetch)."""
+    mnem = "v_mfma_f32_32x32x16_" + dt
+    nx = (j_slot + 1) % 4
+    mf = []
+    if pv:
+        for f in range(16):
+            ks, d = f // 4, f % 4
+            mf.append((("V", f), f"{mnem} {otup(d)}, {vtup(f % VS)}, {ptup(ks)}, {otup(d)}"))
+    if qk:
+        for f in range(16):
+            s, kt = f // 2, f % 2
+            mf.append((("K", f), f"{mnem} {sv(kt)}, {ktup(f % KS)}, {qtup(s)}, {sv(kt) if s else '0'}"))
+    G = len(mf)
+    first, last = {}, {}
+    for g, (tag, _) in enumerate(mf):
+        first.setdefault(tag, g)
+        last[tag] = g
+    reads = []
+    if pv:
+        for f in range(NVPRE, 16):
+            lo = last[("V", f - VS)] + 2 if f >= VS else 0
+            g = min(max(lo, first[("V", f)] - LEAD, 0), first[("V", f)] - 1)
+            reads.append((g, 1, v_reads(f, j_slot, f % VS), ("V", f)))
+    if qk:
+        for f in range(16):
+            g = max(first[("K", f)] - LEAD, 0)
+            if f >= KS:
+                g = max(g, last[("K", f - KS)] + 2)
+            g = min(g, first[("K", f)] - 1) if first[("K", f)] > 0 else -1
+            reads.append((g, 0, [k_read(f, nx, f % KS)], ("K", f)))
+        for f in range(NVPRE):
+            lo = (last[("V", 16 - VS + f)] + 2) if pv else 0
+            g = max(lo, G - 2 * NVPRE + 2 * f)
+            reads.append((min(g, G), 2 + f, v_reads(f, nx, f), ("N", f)))
+    issued, last_idx = [], {}
+    if pv:
+        for f in range(NVPRE):
+            issued += [("V", f)] * 2
+            last_idx[("V", f)] = len(issued) - 1
+    waited = 0
+    byg = {}
+    for g, o, txt, tag in reads:
+        byg.setdefault(g, []).append((o, txt, tag))
+    out = []
+    for g in range(-1, G + 1):
+        for o, txt, tag in sorted(byg.get(g, []), key=lambda x: x[0]):
+            out += txt
+            issued += [tag] * len(txt)
+            if tag[0] in "KV":
+                last_idx[tag] = len(issued) - 1
+        if 0 <= g < G:
+            tag, text = mf[g]
+            if tag in last_idx and last_idx[tag] >= waited:
+                n = min(len(issued) - last_idx[tag] - 1, 15)
+                out.append(f"s_waitcnt lgkmcnt({n})")
+                waited = len(issued) - n
+            out.append(text)
+    return out
+
+
+def dma_pieces(slot):
+    out = []
+    for w, srd, base in (("K", SKR, 0), ("V", SVR, 4 * TILE)):
+        for i in (0, 1):
+            out.append([f"s_add_u32 m0, %[kdst], {base + slot * TILE + i * 1024}", "s_nop 0",
+                        f"buffer_load_dwordx4 %[dma{i}], s[{srd}:{srd + 3}], 0 offen lds"])
+    return out
+
+
+def dma_advance():
+    out = []
+    for r in (SKR, SVR):
+        out += [f"s_add_u32 s{r}, s{r}, %[kstep]", f"s_addc_u32 s{r + 1}, s{r + 1}, 0",
+                f"s_sub_i32 s{r + 2}, s{r + 2}, %[kstep]", f"s_max_i32 s{r + 2}, s{r + 2}, 0"]
+    return out
+
+
+def softmax(dt, mask):
+    """P = exp2(S c - m) of this lane's 32 scores (masked: keys at or past the lane's limit give
+    0), the tile row sum in LT; 4 scores in flight"""
+    ops = []
+    for v in range(32):
+        t = f"v{TMP + v % 8}"
+        off, dword = value_info(v)
+        ex = [f"v_exp_f32 {t}, {t}"]
+        if mask:
+            ex += [f"v_cmp_lt_i32 vcc, {off}, v{LIM}", f"v_cndmask_b32 {t}, 0, {t}, vcc"]
+        st = [[f"v_fma_f32 {t}, v{SBASE + v}, %[c], v{NM}"], ex,
+              [f"v_mov_b32 v{LT}, {t}" if v == 0 else f"v_add_f32 v{LT}, v{LT}, {t}"]]
+        if v & 1:
+            st[2].append(f"v_cvt_pk_{dt}_f32 v{PBASE + dword}, v{TMP + (v - 1) % 8}, {t}")
+        for k, txt in enumerate(st):
+            ops.append((v + 2 * k, v, txt))
+    out = []
+    for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1])):
+        out += txt
+    return out + ["s_nop 0"]
+
+
+def row_max(dst):
+    """masked max of this lane's row over the tile's 64 keys (both lane halves) -> dst"""
+    t2, ninf = f"v{MISC + 1}", f"v{MISC + 3}"
+    out = [f"v_mov_b32 {ninf}, 0xff800000", f"v_mov_b32 {dst}, {ninf}"]
+    for v in range(32):
+        off, _ = value_info(v)
+        out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM}",
+                f"v_cndmask_b32 {t2}, {ninf}, v{SBASE + v}, vcc",
+                f"v_max_f32 {dst}, {dst}, {t2}"]
+    return out + [f"v_mov_b32 {t2}, {dst}", "s_nop 1", f"v_permlane32_swap_b32 {dst}, {t2}",
+                  "s_nop 1", f"v_max_f32 {dst}, {dst}, {t2}"]
+
+
+def first_max():
+    """m = the masked max of tile 0 (in log2 units: NM = -c max, 0 for a row with no key)"""
+    mx, t2 = f"v{MISC}", f"v{MISC + 1}"
+    return ["s_nop 7", "s_nop 7", "s_nop 3"] + row_max(mx) + [
+        f"v_mul_f32_e64 {t2}, -%[c], {mx}",
+        f"v_cmp_lg_f32 vcc, 0xff800000, {mx}",
+        f"v_cndmask_b32 v{NM}, 0, {t2}, vcc"]
+
+
+def redo_block(dt, uid):
+    """rare path: the tile's scores passed the threshold against the reference m.  Take the
+    tile's true (masked) max, m_new = max(m, c max); O and l scaled by 2^(m - m_new); the
+    softmax redone against m_new (its row sum replaces LT).  Returns through SRA."""
+    mx, t2, alpha = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}"
+    out = [f".Lredo_{uid}:", "s_nop 7", "s_nop 7", "s_nop 3"] + row_max(mx)
+    out += [f"v_mul_f32 {t2}, %[c], {mx}",
+            f"v_max_f32_e64 {t2}, {t2}, -v{NM}",          # m_new = max(m_ref, c max)
+            f"v_add_f32 {alpha}, v{NM}, {t2}",             # m_new - m_ref >= 0
+            f"v_exp_f32_e64 {alpha}, -{alpha}",
+            f"v_mul_f32 v{NM}, -1.0, {t2}",
+            "s_nop 0",
+            f"v_mul_f32 v{LRUN}, v{LRUN}, {alpha}"]
+    for i in range(64):
+        t = f"v{TMP + i % 8}"
+        out += [f"v_accvgpr_read_b32 {t}, a{ABASE_O + i}", f"v_mul_f32 {t}, {t}, {alpha}",
+                f"v_accvgpr_write_b32 a{ABASE_O + i}, {t}"]
+    out += ["s_nop 1"] + softmax(dt, True)
+    return out + ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+
+
+def redo_check(uid, tag):
+    """(inline part, stub): any lane's tile row sum past 2^slack -> the rare path; then l += LT"""
+    inline = [f"v_cmp_lt_f32 vcc, %[thr], v{LT}", "s_nop 1", f"s_cbranch_vccnz .Lrc{tag}_{uid}",
+              f".Lnr{tag}_{uid}:", f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}"]
+    stub = [f".Lrc{tag}_{uid}:", f"s_getpc_b64 s[{SRA}:{SRA + 1}]", f".Lpc{tag}_{uid}:",
+            f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
+            *addc_ret(SRA + 1, f".Lnr{tag}_{uid}", f".Lpc{tag}_{uid}", True),
+            f"s_branch .Lredo_{uid}"]
+    if "noredo" in ABL:
+        return [f"v_add_f32 v{LRUN}, v{LRUN}, v{LT}"], []
+    return inline, stub
+
+
+def v_phase(dt, slot, kind, uid, tag):
+    """V phase: kind 'u' unmasked softmax, 'm' masked, 'n' none; DMA of the tile in slot.
+    Returns (inline, out-of-line stubs)."""
+    pieces = dma_pieces(slot)
+    if kind == "n" or ("nosm" in ABL and kind == "u"):
+        return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
+    sm = softmax(dt, kind == "m")
+    if DMAMIX:
+        out = pieces[0] + ["s_nop 7", "s_nop 7"]        # last QK^T results -> VALU
+        # the other 3 pieces spread through the softmax
+        step = len(sm) // 4
+        for n, pc in enumerate(pieces[1:]):
+            at = (n + 1) * step + 3 * n
+            sm[at:at] = pc
+    else:
+        out = sum(pieces, []) + ["s_nop 7", "s_nop 7"]
+    out += sm
+    inl, stub = redo_check(uid, tag)
+    out += inl + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"]
+    return out, stub
+
+
+def epilogue_core(dt):
+    """O / l -> dt rows (16-byte stores after a permlane32 exchange), LSE; the row's two lane
+    halves' sums combined first"""
+    inv, L, t, lse, cls, pinf = (f"v{TMP + i}" for i in range(6))
+    out = [f"v_mov_b32 {pinf}, 0x7f800000",
+           f"v_mov_b32 {t}, v{LRUN}", "s_nop 1", f"v_permlane32_swap_b32 v{LRUN}, {t}", "s_nop 1",
+           f"v_add_f32 {L}, v{LRUN}, {t}", f"v_rcp_f32 {inv}, {L}", f"v_log_f32 {lse}, {L}",
+           f"v_mov_b32 {cls}, 0x63", f"v_cmp_class_f32 vcc, {L}, {cls}",
+           f"v_cndmask_b32_e64 {inv}, {inv}, 1.0, vcc", f"v_sub_f32 {lse}, {lse}, v{NM}",
+           f"v_mul_f32 {lse}, 0x3f317218, {lse}", f"v_cndmask_b32 {lse}, {lse}, {pinf}, vcc",
+           f"buffer_store_dword {lse}, %[loff], %[lsrd], 0 offen"]
+    n = 0
+    for d in range(4):
+        for gp in (0, 2):
+            vb = 0 if n % 2 == 0 else 16          # two alternating register sets in S
+            n += 1
+            vals = [f"v{vb + k}" for k in range(8)]
+            w0 = vb + 8
+            src = [f"a{ABASE_O + 16 * d + 4 * gp + k}" for k in range(8)]
+            out += [f"v_accvgpr_read_b32 {vals[k]}, {src[k]}" for k in range(8)]
+            out += [f"v_mul_f32 {vals[k]}, {vals[k]}, {inv}" for k in range(8)]
+            out += [f"v_cvt_pk_{dt}_f32 v{w0 + k}, {vals[2 * k]}, {vals[2 * k + 1]}" for k in range(4)]
+            out += ["s_nop 1", f"v_permlane32_swap_b32 v{w0}, v{w0 + 2}",
+                    f"v_permlane32_swap_b32 v{w0 + 1}, v{w0 + 3}", "s_nop 1",
+                    f"buffer_store_dwordx4 v[{w0}:{w0 + 3}], %[ooff], %[osrd], 0 offen offset:{64 * d + 16 * gp}",
+                    "s_nop 1"]
+    return out
+
+
+def epilogue(dt):
+    """once per wave: the rows' epilogue (marks SST)"""
+    return [f"s_mov_b32 s{SST}, 1", "s_nop 7", "s_nop 7", "s_nop 3"] + epilogue_core(dt)
+
+
+N_EPI_STORES = 9       # 8 O row stores + the LSE store
+
+
+def group_program(dt, grp):
+    """the phase program of group A (grp 0) or B (grp 1); uid keeps their labels apart"""
+    uid = f"{'AB'[grp]}_%="
+    m_wait = ["s_waitcnt vmcnt(0)"] if grp else []          # B publishes after its M phases
+    v_wait = [] if grp else ["s_waitcnt vmcnt(4)"]          # A publishes after its V phases
+    bar = ["s_barrier"]
+    out, tail = [], []
+    if grp:
+        out += bar                                          # B runs one phase behind A
+    # M(-1) = QK(0) (waves with a visible key), V(-1) = tile-0 max + softmax(0) (masked) + DMA
+    out += [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
+    out += m_phase(dt, 3, pv=False) + m_wait + bar
+    v, stub = v_phase(dt, 2, "m", uid, "f")
+    out += first_max() + v + v_wait + bar
+    tail += stub
+    out += [f"s_branch .Lloop_{uid}", f".Lni_{uid}:"]
+    # (no visible key: the same barriers and DMA duty)
+    out += m_wait + bar
+    v, _ = v_phase(dt, 2, "n", uid, "fi")
+    out += v + v_wait + bar
+    out += [f".Lloop_{uid}:", f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
+            f"s_cbranch_scc1 .Lexit_{uid}"]
+    for ph in range(4):
+        vslot = (ph + 3) % 4                                 # the tile j+3 this V phase loads
+        out.append(f".Lph{ph}_{uid}:")
+        out += [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
+                f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
+                f"s_cbranch_scc0 .Lm{ph}_{uid}"]
+        # unmasked step (inline)
+        out += m_phase(dt, ph) + m_wait + bar
+        v, stub = v_phase(dt, vslot, "u", uid, f"u{ph}")
+        out += v + v_wait + bar
+        tail += stub
+        out += [f".Lnx{ph}_{uid}:", f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
+                f"s_cbranch_scc1 .Lexit_{uid}"]
+        # masked step
+        tail.append(f".Lm{ph}_{uid}:")
+        tail += m_phase(dt, ph) + m_wait + bar
+        v, stub = v_phase(dt, vslot, "m", uid, f"m{ph}")
+        tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"] + stub
+        # j >= t_w: the last step (PV(j), then the epilogue beside the DMA) or an idle one
+        tail += [f".Lx{ph}_{uid}:", f"s_cmp_eq_u32 s{SJ}, %[tw]", f"s_cbranch_scc0 .Li{ph}_{uid}"]
+        tail += m_phase(dt, ph, qk=False) + m_wait + bar
+        v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
+        # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
+        tail += v + epilogue(dt)
+        tail += ([] if grp else [f"s_waitcnt vmcnt({4 + N_EPI_STORES})"]) + bar
+        tail += [f"s_branch .Lnx{ph}_{uid}"]
+        tail.append(f".Li{ph}_{uid}:")
+        tail += m_wait + bar
+        v, _ = v_phase(dt, vslot, "n", uid, f"i{ph}")
+        tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"]
+    out.append(f"s_branch .Lph0_{uid}")
+    out.append(f".Lexit_{uid}:")
+    if not grp:
+        out += bar                                          # A's closing phase
+    # rows that never reached a last step (no visible key): their O = 0, LSE = +inf
+    out += [f"s_cmp_eq_u32 s{SST}, 0", f"s_cbranch_scc0 .Ldone_{uid}"] + epilogue(dt)
+    out += [f".Ldone_{uid}:", "s_waitcnt vmcnt(0)", "s_branch .Lend_%="]
+    return out + tail + redo_block(dt, uid)
+
+
+def item_program(dt):
+    out = ["s_waitcnt lgkmcnt(0)",
+           f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LIM}, %[lim]",
+           f"s_mov_b32 s{SST}, 0"]
+    out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
+    out += [f"v_accvgpr_write_b32 a{ABASE_O + i}, 0" for i in range(64)]
+    for r, lo, hi in ((SKR, "kblo", "kbhi"), (SVR, "vblo", "vbhi")):
+        out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
+                f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
+    for slot in (0, 1):                                      # tiles 0 and 1
+        out += sum(dma_pieces(slot), []) + dma_advance()
+    out += ["s_waitcnt vmcnt(4)", "s_barrier"]               # Q and tile 0 landed, published
+    out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
+    out += group_program(dt, 0) + [".LgrpB_%=:"] + group_program(dt, 1) + [".Lend_%=:"]
+    return out
+
+
+SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const int kvbytes, "
+       "const i32x4 qsrd, const i32x4 osrd, const i32x4 lsrd, const int kstep, const int kdst, "
+       "const int ntl, const int tw, const int ew, const int grp, const float c, const float thr, "
+       "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
+       "const int lim, const int qoff, const int ooff, const int loff")
+OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
+       '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
+       '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
+       '[grp] "s"(grp)', '[c] "s"(c)', '[thr] "s"(thr)',
+       '[kb0] "v"(kb0)', '[kb1] "v"(kb1)', '[vb0] "v"(vb0)', '[vb1] "v"(vb1)',
+       '[dma0] "v"(dma0)', '[dma1] "v"(dma1)', '[lim] "v"(lim)', '[qoff] "v"(qoff)',
+       '[ooff] "v"(ooff)', '[loff] "v"(loff)']
+
+
+def clobbers():
+    regs = [f'"v{i}"' for i in range(96)] + [f'"a{i}"' for i in range(128)]
+    regs += [f'"s{i}"' for i in range(SKR, SCM + 2)]
+    return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
+
+
+def emit(out=OUT):
+    lines = [
+        "// GENERATED by tools/gen_fwdpp.py -- do not edit by hand.",
+        "// The 8-wave ping-pong D = 128 forward's item body (fmha_fwdpp_kernel.h): one asm statement",
+        "// per dtype with a fixed register map; see the generator's docstring for the schedule.",
+        "#pragma once",
+        '#include "fmha_common.h"',
+        "",
+        "namespace xfa {",
+        "typedef __attribute__((ext_vector_type(4))) int i32x4;",
+        "",
+    ]
+    for dt in ("bf16", "f16"):
+        prog = item_program(dt)
+        prog += GUARDS
+        GUARDS.clear()
+        lines.append(f"__device__ __forceinline__ void fwdpp_item_{dt}({SIG}) {{")
+        lines.append("    asm volatile(")
+        lines += [f'        "{b}\\n"' for b in prog]
+        lines.append("        :")
+        lines.append("        : " + ",\n          ".join(OPS))
+        lines.append(f"        : {clobbers()});")
+        lines.append("}")
+        lines.append("")
+        print(dt, len(prog), "instructions/labels")
+    lines.append("}  // namespace xfa")
+    open(out, "w").write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lead", type=int, default=LEAD, help="gaps an LDS read leads its MFMA")
+    ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
+    ap.add_argument("--no-dmamix", dest="dmamix", action="store_false")
+    ap.add_argument("--out", default=OUT)
+    a = ap.parse_args()
+    LEAD, DMAMIX = a.lead, a.dmamix
+    ABL = set(x for x in a.abl.split(",") if x)
+    emit(a.out)

@@ -384,7 +384,7 @@ int fmha_set_option(const char* name, int value) {
         {"fwd_xcdq", &o.fwd_xcdq, 0, 1},         {"fwd_pipe", &o.fwd_pipe, 0, 2},
         {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
-        {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 1},
+        {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 2},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
         {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
         {"fp8_w4", &o.fp8_w4, 0, 1},           {"comb_row", &o.comb_row, 0, 1},

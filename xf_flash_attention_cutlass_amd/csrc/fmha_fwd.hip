@@ -5,6 +5,7 @@
 #include "fmha_fwd_kernel.h"
 #if XFA_HD == 128
 #include "fmha_fwd4_kernel.h"
+#include "fmha_fwdpp_kernel.h"
 #endif
 #include "fmha_decode_kernel.h"
 #include "fmha_sdmask_kernel.h"
@@ -140,7 +141,30 @@ static bool fwd4_eligible(const FwdParams& p) {
            !(p.softcap_pre > 0.f) && !p.block_table && !p.kv_fp8 && !p.leftpad_k && !p.drop;
 }
 
+// 8-wave ping-pong forward (fmha_fwdpp_kernel.h): the same items, schedules and eligibility
+static hipError_t launch_fwdpp(const FwdParams& p, hipStream_t st) {
+    const int n_mb = (p.seqlen_q * p.group + kFwdppRows - 1) / kFwdppRows;
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    dim3 grid(p.b * p.hk, n_mb, 1);
+    const int items = p.b * p.hk * n_mb;
+    const int slots = p.num_cus;
+    if (p.persist_per_cu > 0 && items > slots) {
+        pp.persistent = p.work_ctr ? 3 : (p.order == 1 && slots % 8 == 0) ? 2 : 1;
+        pp.xcd_queues = p.work_ctr && p.xcdq && slots % 8 == 0 && p.b * p.hk >= 8;
+        grid = dim3(slots, 1, 1);
+    }
+    constexpr bool BF = std::is_same<elem_t, __bf16>::value;
+    static std::atomic<unsigned long long> attr_done{0};
+    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem); });
+    note_launch("fmha_fwdpp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
+    hipLaunchKernelGGL((fmha_fwdpp_kernel<BF>), grid, dim3(512), kFwdppSmem, st, pp);
+    return hipGetLastError();
+}
+
 static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
+    if (p.fwd4 == 2) return launch_fwdpp(p, st);
     const int n_mb = (p.seqlen_q * p.group + kFwd4Rows - 1) / kFwd4Rows;
     FwdParams pp = p;
     pp.n_mblocks = n_mb;

@@ -1,0 +1,215 @@
+// fmha_fwdpp_kernel.h — 8-wave "ping-pong" forward for D = 128 (two waves per SIMD, 32 query
+// rows per wave).
+//
+// Replaces the reference's `compute_attn_1rowblock_splitkv` (flash_fwd_kernel_hip.h:585-1283)
+// for the shapes the 4-wave kernel (fmha_fwd4_kernel.h) runs — dense and varlen, D = 128, bf16 /
+// fp16, causal / right window / none, one split — with the same math and item (256 query rows
+// of one (batch x kv head)), re-structured for two waves per SIMD:
+//
+//  * wave w owns rows 32w .. 32w + 31 of the item; waves w and w + 4 share a SIMD;
+//  * a wave alternates an MFMA phase (PV of tile j, QK^T of tile j+1) and a VALU phase (softmax
+//    of tile j+1, its share of the LDS-DMA of tile j+3), each closed by a barrier, and waves 4-7
+//    run one phase behind waves 0-3: on every SIMD one wave issues MFMAs while the other issues
+//    VALU / DMA (tools/gen_fwdpp.py generates the item body, fmha_fwdpp_body.h);
+//  * no row max in the loop (P against tile 0's max, a rare redo past 2^fwd_slack), as the
+//    4-wave kernel.
+// This file computes the item geometry (SRDs, per-lane offsets, the wave's last / first-masked
+// tiles) and runs the persistent item schedules of fmha_fwd4_kernel.h.
+#pragma once
+
+#include "fmha_common.h"
+#ifdef XFA_FWDPP_BODY
+#include XFA_FWDPP_BODY         // an A/B variant of the generated body (tools/fwdpp_variants.sh)
+#else
+#include "fmha_fwdpp_body.h"
+#endif
+
+namespace xfa {
+
+constexpr int kFwdppRows = 256;            // query rows per workgroup (8 waves x 32)
+constexpr int kFwdppTile = 128 * 64 * 2;   // bytes of one K (or V) tile at D = 128
+constexpr int kFwdppVReg = 4 * kFwdppTile;
+constexpr int kFwdppSmem = 8 * kFwdppTile; // 4 K + 4 V slots, 128 KiB
+
+__device__ __forceinline__ i32x4 fwdpp_srd(const void* base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xFFFF);
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+
+// One (batch x kv head, 256-row query block) item.
+template <bool BF16>
+__device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const int bh, const int m_block) {
+    constexpr int HD = 128;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));       // item-local: not hoisted out of the persistent loop
+    const int lane = tid & 63;
+    const int lr = lane & 31;
+    const int hh = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const int bidx = bh / p.hk;
+    const int hk_i = bh - bidx * p.hk;
+    int q_off = 0, sq = p.seqlen_q, k_off = 0, sk = p.seqlen_k;
+    if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
+    if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
+    if (p.seqused_k) sk = p.seqused_k[bidx];
+    const int G = p.group;
+    const int rows_total = sq * G;
+    const int row0 = m_block * kFwdppRows;
+    if (row0 >= rows_total) return;    // workgroup-uniform
+    const int diag = sk - sq;
+    auto lim_r = [&](int pos) { return p.wr >= 0 ? min(sk, pos + diag + p.wr + 1) : sk; };
+
+    // key tiles of the workgroup: [0, ntl)
+    const int pos_hi = (min(row0 + kFwdppRows, rows_total) - 1) / G;
+    const int n_hi = sk > 0 ? lim_r(pos_hi) : 0;
+    const int ntl = n_hi > 0 ? (n_hi + kBlockN - 1) / kBlockN : 0;
+
+    // this wave: rows wrow0 .. wrow0 + 31; last tile t_w; tiles >= e_w need the edge mask
+    const int wrow0 = row0 + 32 * wave;
+    int t_w = -1, e_w = 1 << 30;
+    if (wrow0 < rows_total && ntl > 0) {
+        const int wp_lo = wrow0 / G, wp_hi = (min(wrow0 + 32, rows_total) - 1) / G;
+        const int lr_hi = lim_r(wp_hi), lr_lo = lim_r(wp_lo);
+        t_w = lr_hi > 0 ? min(ntl, (lr_hi + kBlockN - 1) / kBlockN) - 1 : -1;
+        e_w = lr_lo > 0 ? lr_lo / kBlockN : 0;
+    }
+    t_w = __builtin_amdgcn_readfirstlane(t_w);
+    e_w = __builtin_amdgcn_readfirstlane(e_w);
+
+    // this lane's row
+    const int row = wrow0 + lr;
+    const bool ok = row < rows_total;
+    const int pos = ok ? row / G : 0;
+    const int head = hk_i * G + (ok ? row - pos * G : 0);
+    const int qoff = ok ? (pos * (int)p.q_row + head * (int)p.q_head) * 2 + 16 * hh : kOOB;
+    const int ooff = ok ? (pos * (int)p.o_row + head * (int)p.o_head) * 2 + 16 * hh : kOOB;
+    const int loff = (ok && hh == 0) ? (int)(head * p.lse_head + pos) * 4 : kOOB;
+    // key limit of tile 0 for this lane's keys (offset 4*hh folded in); other rows: none
+    const int lim = (ok ? lim_r(pos) : sk) - 4 * hh;
+
+    if (ntl <= 0) {
+        // no visible key for any row: O = 0, LSE = +inf (the reference's empty-row output)
+        typedef __attribute__((ext_vector_type(4))) unsigned u4;
+        char* oseq = reinterpret_cast<char*>(p.o) + ((int64_t)bidx * p.o_batch + (int64_t)q_off * p.o_row) * 2;
+        if (ooff != kOOB) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) *reinterpret_cast<u4*>(oseq + ooff + 32 * c) = u4{0, 0, 0, 0};
+            if (p.lse && hh == 0) p.lse[(int64_t)bidx * p.lse_batch + q_off + loff / 4] = INFINITY;
+        }
+        return;
+    }
+
+    // SRDs: Q / O / LSE of this sequence; K / V of this sequence and kv head, their range ending
+    // at the workgroup's last key tile (the ring's DMA past it reads zeros and moves no bytes)
+    const char* qseq = reinterpret_cast<const char*>(p.q) + ((int64_t)bidx * p.q_batch + (int64_t)q_off * p.q_row) * 2;
+    char* oseq = reinterpret_cast<char*>(p.o) + ((int64_t)bidx * p.o_batch + (int64_t)q_off * p.o_row) * 2;
+    const uint32_t qbytes = (uint32_t)(((int64_t)(sq - 1) * p.q_row + (int64_t)(p.h - 1) * p.q_head + HD) * 2);
+    const uint32_t obytes = (uint32_t)(((int64_t)(sq - 1) * p.o_row + (int64_t)(p.h - 1) * p.o_head + HD) * 2);
+    const i32x4 qsrd = fwdpp_srd(qseq, qbytes), osrd = fwdpp_srd(oseq, obytes);
+    const float* lseq = p.lse ? p.lse + (int64_t)bidx * p.lse_batch + q_off : p.lse;
+    const int64_t lbytes = p.lse ? ((int64_t)(p.h - 1) * p.lse_head + sq) * 4 : 0;
+    const i32x4 lsrd = fwdpp_srd(lseq, (uint32_t)min(lbytes, (int64_t)kOOB - 1));
+    const int k_row = (int)p.k_row;
+    const char* kseq = reinterpret_cast<const char*>(p.k) +
+                       ((int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row + (int64_t)hk_i * p.k_head) * 2;
+    const char* vseq = reinterpret_cast<const char*>(p.v) +
+                       ((int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row + (int64_t)hk_i * p.v_head) * 2;
+    const int nk = min(sk, ntl * kBlockN);
+    const int kvbytes = __builtin_amdgcn_readfirstlane((int)(((nk - 1) * k_row + HD) * 2));
+    const int kblo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)kseq);
+    const int kbhi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)kseq >> 32) & 0xFFFF);
+    const int vblo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)vseq);
+    const int vbhi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)vseq >> 32) & 0xFFFF);
+
+    // LDS-DMA: wave w loads 8-row block w of every K / V tile, pieces i = chunks 8i .. 8i+7 of
+    // the kv_off image (lane l lands at +16 l); K and V share the offsets (k_row == v_row)
+    const int r = 8 * wave + lr / 4;
+    const int cch = 4 * hh + ((lane & 3) ^ ((r >> 2) & 3));
+    const int dma0 = r * k_row * 2 + cch * 16;
+    // LDS read bases (kv_off image, slot 0; the ring slots are immediate offsets)
+    const int sbase = (int)(size_t)smem;
+    int kb[2], vb[2];
+    {
+        const int q4 = (lane & 15) >> 2;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            kb[u] = sbase + kv_off<HD>(lr, 2 * u + hh);
+            const int rr = 8 * u + 4 * hh + q4;
+            const int col = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+            vb[u] = sbase + kFwdppVReg + kv_off<HD>(rr, col >> 3) + 8 * ((col >> 2) & 1);
+        }
+    }
+    const int kstep = __builtin_amdgcn_readfirstlane(kBlockN * k_row * 2);
+    const int kdst = __builtin_amdgcn_readfirstlane(sbase + wave * 2048);
+    const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);
+    const float thr = __builtin_amdgcn_exp2f(p.max_slack);
+    if constexpr (BF16)
+        fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff);
+    else
+        fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff);
+}
+
+// Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
+// (n-1-i, i) row-block pairs (dense) or per-XCD dynamic queues (varlen).
+template <bool BF16>
+__global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int s_claim[2];
+    const int nbh = p.b * p.hk;
+    const int g = gridDim.x;
+    for (int k = 0;; ++k) {
+        int bh, m_block;
+        if (p.persistent == 2) {
+            const int nm = p.n_mblocks, npair = (nm + 1) >> 1;
+            const int bid = (int)blockIdx.x;
+            const int v = (bid & 7) * (g >> 3) + (bid >> 3);
+            const int q = (k >> 1) * g + v;
+            if (q >= nbh * npair) break;
+            bh = q / npair;
+            const int i = q - bh * npair;
+            m_block = (k & 1) ? i : nm - 1 - i;
+            if ((k & 1) && i == nm - 1 - i) continue;
+        } else if (p.persistent == 1) {
+            const int lin = k * g + ((k & 1) ? g - 1 - (int)blockIdx.x : (int)blockIdx.x);
+            if (lin >= nbh * p.n_mblocks) break;
+            bh = lin % nbh;
+            m_block = p.n_mblocks - 1 - lin / nbh;
+        } else if (p.persistent == 3) {
+            const int x = p.xcd_queues ? (int)(blockIdx.x & 7) : 0;
+            const int nq = p.xcd_queues ? (nbh - x + 7) >> 3 : nbh;
+            if (threadIdx.x == 0) s_claim[k & 1] = atomicAdd(p.work_ctr + 2 + x, 1);
+            __syncthreads();
+            const int q = s_claim[k & 1];
+            if (q >= nq * p.n_mblocks) break;
+            if (p.xcd_queues) {
+                bh = x + 8 * (q / p.n_mblocks);
+                m_block = p.n_mblocks - 1 - q % p.n_mblocks;
+            } else {
+                bh = q % nq;
+                m_block = p.n_mblocks - 1 - q / nq;
+            }
+        } else {
+            if (k > 0) break;
+            bh = blockIdx.x;
+            m_block = gridDim.y - 1 - blockIdx.y;
+        }
+        fwdpp_item<BF16>(p, smem, bh, m_block);
+    }
+    if (p.persistent == 3 && threadIdx.x == 0) {
+        const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+        if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {
+            for (int i = 2; i < 10; ++i) atomicExch(p.work_ctr + i, 0);
+            atomicExch(p.work_ctr + 1, 0);
+        }
+    }
+}
+
+}  // namespace xfa

@@ -14,7 +14,10 @@ namespace xfa {
 // parity suite runs under any of them via XFA_TEST_OPTIONS).  Atomic: a launch on another
 // thread reads each knob once, as a whole value.
 struct Options {
-    std::atomic<int> fwd_w4{1};          // 4-wave D = 128 forward (fmha_fwd4_kernel.h) where eligible
+    std::atomic<int> fwd_w4{2};          // D = 128 forward where eligible: 2 the 8-wave ping-pong
+                                         // kernel (fmha_fwdpp_kernel.h; round 5, same box: C2 causal
+                                         // +2-3 %, C4 +3 %, non-causal equal), 1 the 4-wave kernel
+                                         // (fmha_fwd4_kernel.h), 0 neither (8-wave fmha_fwd_kernel)
     std::atomic<int> fp8_w4{1};          // 4-wave fp8 forward (fmha_fwd8w_kernel.h) where eligible
                                          // (C2 shape, same box: 1610 vs 1576 TFLOP/s causal, 1852 vs
                                          // 1799 non-causal)
