@@ -59,13 +59,14 @@ def _check(xfa, b, h, hk, sq, sk, causal=False, window=(-1, -1), seed=0, out_dty
 
 
 def _assert_fp8_w4():
-    """launches without a left window run the 4-wave fp8 kernel (fp8_w4 = 1, the default; the
-    8-wave one under XFA_TEST_OPTIONS=fp8_w4=0)"""
+    """launches without a left window run the generated fp8 kernel fp8_w4 selects (2 the ping-pong
+    kernel, 1 the 4-wave kernel; 0, under XFA_TEST_OPTIONS=fp8_w4=0, the 8-wave compiler-scheduled
+    one)"""
     from xf_flash_attention_cutlass_amd import capi
     L = capi.lib()
     kern = L.fmha_last_kernel().decode()
-    want = "fmha_fwd8w_kernel" if L.fmha_get_option(b"fp8_w4") else "fmha_fwd_fp8_kernel"
-    assert kern.startswith(want), kern
+    want = {0: "fmha_fwd_fp8_kernel", 1: "fmha_fwd8w_kernel", 2: "fmha_fwd8pp_kernel"}
+    assert kern.startswith(want[L.fmha_get_option(b"fp8_w4")]), kern
 
 
 @pytest.mark.parametrize("causal", [False, True])

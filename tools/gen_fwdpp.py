@@ -58,6 +58,12 @@ ABASE_O, ABASE_Q, ABASE_K, VBASE_V = 0, 64, 96, 64
 SKR, SVR = 80, 84
 SJ, ST, SST, SRA, SCM = 88, 89, 90, 92, 94
 ABL = set()            # timing ablations (results INVALID): nosm noredo
+# (tools/gen_fwd8pp.py reuses this generator's phase program for the fp8 kernel: it rebinds the
+#  operand-specific functions below and these parameters)
+XDL_NOPS = ["s_nop 7", "s_nop 7", "s_nop 3"]   # last MFMA write -> VALU read of O / S
+VPH_NOPS = ["s_nop 7", "s_nop 7"]              # (a V phase: after its first DMA piece)
+NPIECE = 4             # LDS-DMA pieces per wave per tile (A's publish wait keeps them in flight)
+EPI_SCALE = None       # an SGPR operand O is also scaled by in the epilogue (fp8: %[vsc])
 DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax (else all first)
 
 GUARDS = []            # assembler checks of the return-address signs, after the whole program
@@ -231,7 +237,7 @@ def row_max(dst):
 def first_max():
     """m = the masked max of tile 0 (in log2 units: NM = -c max, 0 for a row with no key)"""
     mx, t2 = f"v{MISC}", f"v{MISC + 1}"
-    return ["s_nop 7", "s_nop 7", "s_nop 3"] + row_max(mx) + [
+    return XDL_NOPS + row_max(mx) + [
         f"v_mul_f32_e64 {t2}, -%[c], {mx}",
         f"v_cmp_lg_f32 vcc, 0xff800000, {mx}",
         f"v_cndmask_b32 v{NM}, 0, {t2}, vcc"]
@@ -242,7 +248,7 @@ def redo_block(dt, uid):
     tile's true (masked) max, m_new = max(m, c max); O and l scaled by 2^(m - m_new); the
     softmax redone against m_new (its row sum replaces LT).  Returns through SRA."""
     mx, t2, alpha = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}"
-    out = [f".Lredo_{uid}:", "s_nop 7", "s_nop 7", "s_nop 3"] + row_max(mx)
+    out = [f".Lredo_{uid}:"] + XDL_NOPS + row_max(mx)
     out += [f"v_mul_f32 {t2}, %[c], {mx}",
             f"v_max_f32_e64 {t2}, {t2}, -v{NM}",          # m_new = max(m_ref, c max)
             f"v_add_f32 {alpha}, v{NM}, {t2}",             # m_new - m_ref >= 0
@@ -279,14 +285,14 @@ def v_phase(dt, slot, kind, uid, tag):
         return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
     sm = softmax(dt, kind == "m")
     if DMAMIX:
-        out = pieces[0] + ["s_nop 7", "s_nop 7"]        # last QK^T results -> VALU
-        # the other 3 pieces spread through the softmax
-        step = len(sm) // 4
+        out = pieces[0] + VPH_NOPS                      # last QK^T results -> VALU
+        # the other pieces spread through the softmax
+        step = len(sm) // len(pieces)
         for n, pc in enumerate(pieces[1:]):
             at = (n + 1) * step + 3 * n
             sm[at:at] = pc
     else:
-        out = sum(pieces, []) + ["s_nop 7", "s_nop 7"]
+        out = sum(pieces, []) + VPH_NOPS
     out += sm
     inl, stub = redo_check(uid, tag)
     out += inl + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"]
@@ -301,7 +307,10 @@ def epilogue_core(dt):
            f"v_mov_b32 {t}, v{LRUN}", "s_nop 1", f"v_permlane32_swap_b32 v{LRUN}, {t}", "s_nop 1",
            f"v_add_f32 {L}, v{LRUN}, {t}", f"v_rcp_f32 {inv}, {L}", f"v_log_f32 {lse}, {L}",
            f"v_mov_b32 {cls}, 0x63", f"v_cmp_class_f32 vcc, {L}, {cls}",
-           f"v_cndmask_b32_e64 {inv}, {inv}, 1.0, vcc", f"v_sub_f32 {lse}, {lse}, v{NM}",
+           f"v_cndmask_b32_e64 {inv}, {inv}, 1.0, vcc"]
+    if EPI_SCALE:
+        out.append(f"v_mul_f32 {inv}, {EPI_SCALE}, {inv}")
+    out += [f"v_sub_f32 {lse}, {lse}, v{NM}",
            f"v_mul_f32 {lse}, 0x3f317218, {lse}", f"v_cndmask_b32 {lse}, {lse}, {pinf}, vcc",
            f"buffer_store_dword {lse}, %[loff], %[lsrd], 0 offen"]
     n = 0
@@ -324,7 +333,7 @@ def epilogue_core(dt):
 
 def epilogue(dt):
     """once per wave: the rows' epilogue (marks SST)"""
-    return [f"s_mov_b32 s{SST}, 1", "s_nop 7", "s_nop 7", "s_nop 3"] + epilogue_core(dt)
+    return [f"s_mov_b32 s{SST}, 1"] + XDL_NOPS + epilogue_core(dt)
 
 
 N_EPI_STORES = 9       # 8 O row stores + the LSE store
@@ -334,7 +343,7 @@ def group_program(dt, grp):
     """the phase program of group A (grp 0) or B (grp 1); uid keeps their labels apart"""
     uid = f"{'AB'[grp]}_%="
     m_wait = ["s_waitcnt vmcnt(0)"] if grp else []          # B publishes after its M phases
-    v_wait = [] if grp else ["s_waitcnt vmcnt(4)"]          # A publishes after its V phases
+    v_wait = [] if grp else [f"s_waitcnt vmcnt({NPIECE})"]  # A publishes after its V phases
     bar = ["s_barrier"]
     out, tail = [], []
     if grp:
@@ -376,7 +385,7 @@ def group_program(dt, grp):
         v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
         # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
         tail += v + epilogue(dt)
-        tail += ([] if grp else [f"s_waitcnt vmcnt({4 + N_EPI_STORES})"]) + bar
+        tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE + N_EPI_STORES})"]) + bar
         tail += [f"s_branch .Lnx{ph}_{uid}"]
         tail.append(f".Li{ph}_{uid}:")
         tail += m_wait + bar

@@ -387,7 +387,7 @@ int fmha_set_option(const char* name, int value) {
         {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 2},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
         {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
-        {"fp8_w4", &o.fp8_w4, 0, 1},           {"comb_row", &o.comb_row, 0, 1},
+        {"fp8_w4", &o.fp8_w4, 0, 2},           {"comb_row", &o.comb_row, 0, 1},
     };
     for (const Knob& k : knobs) {
         if (strcmp(name, k.name)) continue;

@@ -2,6 +2,7 @@
 // bf16 or fp16 output; persistent XCD-paired grid as the bf16 forward.
 #include "fmha_fwd_fp8_kernel.h"
 #include "fmha_fwd8w_kernel.h"
+#include "fmha_fwd8pp_kernel.h"
 #include "fmha_launch.h"
 
 namespace xfa {
@@ -25,6 +26,27 @@ static hipError_t launch_fp8_w4(const FwdParams& p, hipStream_t st) {
     once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8w_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8wSmem); });
     note_launch("fmha_fwd8w_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 256);
     hipLaunchKernelGGL((fmha_fwd8w_kernel<F16>), grid, dim3(256), kFwd8wSmem, st, pp);
+    return hipGetLastError();
+}
+
+// 8-wave ping-pong fp8 forward (fmha_fwd8pp_kernel.h): the same items, schedules, eligibility
+template <bool F16>
+static hipError_t launch_fp8_pp(const FwdParams& p, hipStream_t st) {
+    const int n_mb = (p.seqlen_q * p.group + kFwd8ppRows - 1) / kFwd8ppRows;
+    FwdParams pp = p;
+    pp.n_mblocks = n_mb;
+    pp.persistent = 0;
+    dim3 grid(p.b * p.hk, n_mb, 1);
+    const int items = p.b * p.hk * n_mb;
+    if (p.persist_per_cu > 0 && items > p.num_cus) {
+        pp.persistent = p.work_ctr ? 3 : (p.order == 1 && p.num_cus % 8 == 0) ? 2 : 1;
+        pp.xcd_queues = p.work_ctr && p.xcdq && p.num_cus % 8 == 0 && p.b * p.hk >= 8;
+        grid = dim3(p.num_cus, 1, 1);
+    }
+    static std::atomic<unsigned long long> attr_done{0};
+    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8pp_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8wSmem); });
+    note_launch("fmha_fwd8pp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
+    hipLaunchKernelGGL((fmha_fwd8pp_kernel<F16>), grid, dim3(512), kFwd8wSmem, st, pp);
     return hipGetLastError();
 }
 
@@ -59,6 +81,8 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
 }
 
 hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st) {
+    if (p.fwd4 == 2 && p.k_row == p.v_row && (p.wl < 0 || p.wl >= p.seqlen_k))
+        return out_fp16 ? launch_fp8_pp<true>(p, st) : launch_fp8_pp<false>(p, st);
     if (p.fwd4 && p.k_row == p.v_row && (p.wl < 0 || p.wl >= p.seqlen_k))
         return out_fp16 ? launch_fp8_w4<true>(p, st) : launch_fp8_w4<false>(p, st);
     return out_fp16 ? launch_fp8_t<_Float16>(p, st) : launch_fp8_t<__bf16>(p, st);
