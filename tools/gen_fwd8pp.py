@@ -35,7 +35,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "xf_flash_attention_cutlass_amd", "csrc", "fmha_fwd8pp_body.h")
 
 TILE = 64 * 128        # one fp8 K (or V) tile
-VREG = 4 * TILE
 MNEM = "v_mfma_scale_f32_32x32x64_f8f6f4"
 SC127 = 56
 ABASE_Q, ABASE_K, VBASE_V = 64, 80, 64
@@ -108,7 +107,7 @@ def m_phase(dt, j_slot, pv=True, qk=True):
     the end (the next PV's operands).  On entry with pv, this tile's V^T fragments (16 reads)
     are the only LDS reads in flight."""
     sc = f"v{SC127}, v{SC127} op_sel_hi:[0,0,0]"
-    nx = (j_slot + 1) % 4
+    nx = (j_slot + 1) % pp.RING
     mf = []
     if pv:
         for d in range(4):
@@ -161,7 +160,7 @@ def m_phase(dt, j_slot, pv=True, qk=True):
 def dma_pieces(slot):
     """this wave's K piece and V piece of the tile in slot (8 rows x 128 bytes each)"""
     out = []
-    for op, srd, base in (("dk", pp.SKR, 0), ("dv", pp.SVR, VREG)):
+    for op, srd, base in (("dk", pp.SKR, 0), ("dv", pp.SVR, pp.RING * TILE)):
         out.append([f"s_add_u32 m0, %[kdst], {base + slot * TILE}", "s_nop 0",
                     f"buffer_load_dwordx4 %[{op}], s[{srd}:{srd + 3}], 0 offen lds"])
     return out
@@ -180,9 +179,10 @@ def item_program(dt):
     for r, lo, hi in ((pp.SKR, "kblo", "kbhi"), (pp.SVR, "vblo", "vbhi")):
         out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
                 f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
-    for slot in (0, 1):                                      # tiles 0 and 1
+    for slot in range(pp.DLEAD - 1):                         # tiles 0 .. DLEAD-2
         out += sum(dma_pieces(slot), []) + pp.dma_advance()
-    out += [f"s_waitcnt vmcnt({pp.NPIECE})", "s_barrier"]   # Q and tile 0 landed, published
+    # Q and tile 0 landed, published
+    out += [f"s_waitcnt vmcnt({pp.NPIECE * (pp.DLEAD - 2)})", "s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
     out += pp.group_program(dt, 0) + [".LgrpB_%=:"] + pp.group_program(dt, 1) + [".Lend_%=:"]
     return out
@@ -215,6 +215,7 @@ def emit(out=OUT):
         "",
         "namespace xfa {",
         "typedef __attribute__((ext_vector_type(4))) int i32x4;",
+        f"constexpr int kFwd8ppRing = {pp.RING};          // K / V tile slots the body addresses",
         "",
     ]
     ops = [f'[{o}] "s"({o})' for o in SOPS] + [f'[{o}] "v"({o})' for o in VOPS]
@@ -239,8 +240,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
     ap.add_argument("--no-dmamix", dest="dmamix", action="store_false")
+    ap.add_argument("--ring", type=int, default=pp.RING, help="K / V tile slots in LDS")
+    ap.add_argument("--dlead", type=int, default=pp.DLEAD, help="V(j) loads tile j + dlead")
+    ap.add_argument("--dma-in-m", action="store_true", help="DMA pieces in the MFMA phase")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
+    pp.RING, pp.DLEAD, pp.DMA_IN_M = a.ring, a.dlead, a.dma_in_m
+    assert 3 <= pp.DLEAD < pp.RING
     pp.ABL = set(x for x in a.abl.split(",") if x)
     pp.DMAMIX = a.dmamix
     emit(a.out)

@@ -65,6 +65,10 @@ VPH_NOPS = ["s_nop 7", "s_nop 7"]              # (a V phase: after its first DMA
 NPIECE = 4             # LDS-DMA pieces per wave per tile (A's publish wait keeps them in flight)
 EPI_SCALE = None       # an SGPR operand O is also scaled by in the epilogue (fp8: %[vsc])
 DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax (else all first)
+DMA_IN_M = False       # the DMA pieces ride in the M phase (between MFMAs) instead of the V phase
+RING = 4               # K / V tile slots in LDS
+DLEAD = 3              # V(j) loads tile j + DLEAD (needs RING > DLEAD: B's last read of tile t
+                       # is in global phase 2t+3, A's load of tile t+RING in 2(t+RING-DLEAD)+3)
 
 GUARDS = []            # assembler checks of the return-address signs, after the whole program
 
@@ -108,15 +112,29 @@ def value_info(v):
     return off, ks * 4 + ((r & 7) >> 1)
 
 
+HI = 3                 # with RING > 4, slots >= HI address from the high bases (kh, vh = base +
+                       # HI tiles): a ds_read offset holds 16 bits
+
+
+def lds_base(name, slot_tile):
+    if RING > 4 and slot_tile >= HI:
+        return f"%[{name[0]}h{name[-1]}]", (slot_tile - HI) * TILE
+    return f"%[{name}]", slot_tile * TILE
+
+
 def k_read(f, slot_tile, dst_slot):
     s, kt = f // 2, f % 2
-    return f"ds_read_b128 {ktup(dst_slot)}, %[kb{s & 1}] offset:{slot_tile * TILE + kt * 4 * RB + 512 * (s >> 1)}"
+    b, o = lds_base(f"kb{s & 1}", slot_tile)
+    return f"ds_read_b128 {ktup(dst_slot)}, {b} offset:{o + kt * 4 * RB + 512 * (s >> 1)}"
 
 
 def v_reads(f, slot_tile, dst_slot):
     ks, d = f // 4, f % 4
-    off = slot_tile * TILE + 2 * ks * RB + 512 * d          # (the lane base carries the V ring)
-    return [f"ds_read_b64_tr_b16 {vtup(dst_slot, h)}, %[vb{h}] offset:{off}" for h in (0, 1)]
+    out = []
+    for h in (0, 1):
+        b, o = lds_base(f"vb{h}", slot_tile)                # (the lane base carries the V ring)
+        out.append(f"ds_read_b64_tr_b16 {vtup(dst_slot, h)}, {b} offset:{o + 2 * ks * RB + 512 * d}")
+    return out
 
 
 def m_phase(dt, j_slot, pv=True, qk=True):
@@ -124,7 +142,7 @@ def m_phase(dt, j_slot, pv=True, qk=True):
     (tile j+1) are read at the end.  On entry with pv, this tile's first NVPRE V^T fragments are
     the only LDS reads in flight (the previous M phase's prefetch)."""
     mnem = "v_mfma_f32_32x32x16_" + dt
-    nx = (j_slot + 1) % 4
+    nx = (j_slot + 1) % RING
     mf = []
     if pv:
         for f in range(16):
@@ -184,7 +202,7 @@ def m_phase(dt, j_slot, pv=True, qk=True):
 
 def dma_pieces(slot):
     out = []
-    for w, srd, base in (("K", SKR, 0), ("V", SVR, 4 * TILE)):
+    for w, srd, base in (("K", SKR, 0), ("V", SVR, RING * TILE)):
         for i in (0, 1):
             out.append([f"s_add_u32 m0, %[kdst], {base + slot * TILE + i * 1024}", "s_nop 0",
                         f"buffer_load_dwordx4 %[dma{i}], s[{srd}:{srd + 3}], 0 offen lds"])
@@ -280,11 +298,11 @@ def redo_check(uid, tag):
 def v_phase(dt, slot, kind, uid, tag):
     """V phase: kind 'u' unmasked softmax, 'm' masked, 'n' none; DMA of the tile in slot.
     Returns (inline, out-of-line stubs)."""
-    pieces = dma_pieces(slot)
+    pieces = [] if DMA_IN_M else dma_pieces(slot)
     if kind == "n" or ("nosm" in ABL and kind == "u"):
         return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
     sm = softmax(dt, kind == "m")
-    if DMAMIX:
+    if DMAMIX and pieces:
         out = pieces[0] + VPH_NOPS                      # last QK^T results -> VALU
         # the other pieces spread through the softmax
         step = len(sm) // len(pieces)
@@ -297,6 +315,23 @@ def v_phase(dt, slot, kind, uid, tag):
     inl, stub = redo_check(uid, tag)
     out += inl + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"]
     return out, stub
+
+
+def m_dma(dt, j_slot, slot, **kw):
+    """an M phase (m_phase(dt, j_slot, **kw), or none for j_slot None) carrying the DMA of the
+    tile in slot when DMA_IN_M: each piece right after an MFMA, spread over the phase"""
+    out = [] if j_slot is None else m_phase(dt, j_slot, **kw)
+    if not DMA_IN_M:
+        return out
+    pieces = dma_pieces(slot)
+    at = [i for i, x in enumerate(out) if x.startswith("v_mfma")]
+    if not at:
+        return sum(pieces, []) + out
+    n = len(pieces)
+    for k in reversed(range(n)):
+        i = at[(k * len(at)) // n] + 1
+        out[i:i] = pieces[k]
+    return out
 
 
 def epilogue_core(dt):
@@ -342,33 +377,35 @@ N_EPI_STORES = 9       # 8 O row stores + the LSE store
 def group_program(dt, grp):
     """the phase program of group A (grp 0) or B (grp 1); uid keeps their labels apart"""
     uid = f"{'AB'[grp]}_%="
-    m_wait = ["s_waitcnt vmcnt(0)"] if grp else []          # B publishes after its M phases
-    v_wait = [] if grp else [f"s_waitcnt vmcnt({NPIECE})"]  # A publishes after its V phases
+    # tile t is published at the barrier closing global phase 2t-1: A (after V(t-2)) has loaded
+    # through tile t-2+DLEAD, B (after M(t-2), its loads one phase later) through t-3+DLEAD
+    m_wait = [f"s_waitcnt vmcnt({NPIECE * (DLEAD - (2 if DMA_IN_M else 3))})"] if grp else []
+    v_wait = [] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2)})"]
     bar = ["s_barrier"]
     out, tail = [], []
     if grp:
         out += bar                                          # B runs one phase behind A
     # M(-1) = QK(0) (waves with a visible key), V(-1) = tile-0 max + softmax(0) (masked) + DMA
     out += [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
-    out += m_phase(dt, 3, pv=False) + m_wait + bar
-    v, stub = v_phase(dt, 2, "m", uid, "f")
+    out += m_dma(dt, RING - 1, DLEAD - 1, pv=False) + m_wait + bar
+    v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f")
     out += first_max() + v + v_wait + bar
     tail += stub
     out += [f"s_branch .Lloop_{uid}", f".Lni_{uid}:"]
     # (no visible key: the same barriers and DMA duty)
-    out += m_wait + bar
-    v, _ = v_phase(dt, 2, "n", uid, "fi")
+    out += m_dma(dt, None, DLEAD - 1) + m_wait + bar
+    v, _ = v_phase(dt, DLEAD - 1, "n", uid, "fi")
     out += v + v_wait + bar
     out += [f".Lloop_{uid}:", f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
             f"s_cbranch_scc1 .Lexit_{uid}"]
-    for ph in range(4):
-        vslot = (ph + 3) % 4                                 # the tile j+3 this V phase loads
+    for ph in range(RING):
+        vslot = (ph + DLEAD) % RING                          # the tile j+DLEAD this V phase loads
         out.append(f".Lph{ph}_{uid}:")
         out += [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         # unmasked step (inline)
-        out += m_phase(dt, ph) + m_wait + bar
+        out += m_dma(dt, ph, vslot) + m_wait + bar
         v, stub = v_phase(dt, vslot, "u", uid, f"u{ph}")
         out += v + v_wait + bar
         tail += stub
@@ -376,19 +413,19 @@ def group_program(dt, grp):
                 f"s_cbranch_scc1 .Lexit_{uid}"]
         # masked step
         tail.append(f".Lm{ph}_{uid}:")
-        tail += m_phase(dt, ph) + m_wait + bar
+        tail += m_dma(dt, ph, vslot) + m_wait + bar
         v, stub = v_phase(dt, vslot, "m", uid, f"m{ph}")
         tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"] + stub
         # j >= t_w: the last step (PV(j), then the epilogue beside the DMA) or an idle one
         tail += [f".Lx{ph}_{uid}:", f"s_cmp_eq_u32 s{SJ}, %[tw]", f"s_cbranch_scc0 .Li{ph}_{uid}"]
-        tail += m_phase(dt, ph, qk=False) + m_wait + bar
+        tail += m_dma(dt, ph, vslot, qk=False) + m_wait + bar
         v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
         # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
         tail += v + epilogue(dt)
-        tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE + N_EPI_STORES})"]) + bar
+        tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2) + N_EPI_STORES})"]) + bar
         tail += [f"s_branch .Lnx{ph}_{uid}"]
         tail.append(f".Li{ph}_{uid}:")
-        tail += m_wait + bar
+        tail += m_dma(dt, None, vslot) + m_wait + bar
         v, _ = v_phase(dt, vslot, "n", uid, f"i{ph}")
         tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
@@ -410,9 +447,10 @@ def item_program(dt):
     for r, lo, hi in ((SKR, "kblo", "kbhi"), (SVR, "vblo", "vbhi")):
         out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
                 f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
-    for slot in (0, 1):                                      # tiles 0 and 1
+    for slot in range(DLEAD - 1):                            # tiles 0 .. DLEAD-2
         out += sum(dma_pieces(slot), []) + dma_advance()
-    out += ["s_waitcnt vmcnt(4)", "s_barrier"]               # Q and tile 0 landed, published
+    # Q and tile 0 landed, published
+    out += [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2)})", "s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
     out += group_program(dt, 0) + [".LgrpB_%=:"] + group_program(dt, 1) + [".Lend_%=:"]
     return out
@@ -422,7 +460,8 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const i32x4 qsrd, const i32x4 osrd, const i32x4 lsrd, const int kstep, const int kdst, "
        "const int ntl, const int tw, const int ew, const int grp, const float c, const float thr, "
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
-       "const int lim, const int qoff, const int ooff, const int loff")
+       "const int lim, const int qoff, const int ooff, const int loff, "
+       "const int kh0, const int kh1, const int vh0, const int vh1")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
@@ -448,6 +487,7 @@ def emit(out=OUT):
         "",
         "namespace xfa {",
         "typedef __attribute__((ext_vector_type(4))) int i32x4;",
+        f"constexpr int kFwdppRing = {RING};           // K / V tile slots the body addresses",
         "",
     ]
     for dt in ("bf16", "f16"):
@@ -458,7 +498,8 @@ def emit(out=OUT):
         lines.append("    asm volatile(")
         lines += [f'        "{b}\\n"' for b in prog]
         lines.append("        :")
-        lines.append("        : " + ",\n          ".join(OPS))
+        hi = ['[kh0] "v"(kh0)', '[kh1] "v"(kh1)', '[vh0] "v"(vh0)', '[vh1] "v"(vh1)'] if RING > 4 else []
+        lines.append("        : " + ",\n          ".join(OPS + hi))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
         lines.append("")
@@ -473,8 +514,12 @@ if __name__ == "__main__":
     ap.add_argument("--lead", type=int, default=LEAD, help="gaps an LDS read leads its MFMA")
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
     ap.add_argument("--no-dmamix", dest="dmamix", action="store_false")
+    ap.add_argument("--ring", type=int, default=RING, help="K / V tile slots in LDS")
+    ap.add_argument("--dlead", type=int, default=DLEAD, help="V(j) loads tile j + dlead")
+    ap.add_argument("--dma-in-m", action="store_true", help="DMA pieces in the MFMA phase")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
-    LEAD, DMAMIX = a.lead, a.dmamix
+    LEAD, DMAMIX, RING, DLEAD, DMA_IN_M = a.lead, a.dmamix, a.ring, a.dlead, a.dma_in_m
+    assert 3 <= DLEAD < RING <= 5
     ABL = set(x for x in a.abl.split(",") if x)
     emit(a.out)

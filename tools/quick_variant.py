@@ -24,10 +24,14 @@ def main():
     tmp = tempfile.mkdtemp(prefix=f"xfa_{name}_")
     repl = {}
     for spec in objs:
-        kind, hd, dt = spec.split(":")
+        if ":" in spec:
+            kind, hd, dt = spec.split(":")
+            out = os.path.join(tmp, f"fmha_{kind}_hd{hd}_{dt}.o")
+            defs = [f"-DXFA_HD={hd}", f"-DXFA_DTN={dt}", f"-DXFA_DT_BF16={1 if dt == 'bf16' else 0}"]
+        else:                                 # a one-object kind (fwd_fp8)
+            kind, defs = spec, []
+            out = os.path.join(tmp, f"fmha_{kind}.o")
         src = os.path.join(build.CSRC, f"fmha_{kind}.hip")
-        out = os.path.join(tmp, f"fmha_{kind}_hd{hd}_{dt}.o")
-        defs = [f"-DXFA_HD={hd}", f"-DXFA_DTN={dt}", f"-DXFA_DT_BF16={1 if dt == 'bf16' else 0}"]
         cmd = [build.HIPCC, *build.HIP_FLAGS, *flags, *defs, "-c", src, "-o", out]
         subprocess.run(cmd, check=True)
         repl[os.path.basename(out)] = out

@@ -9,11 +9,17 @@
 #pragma once
 
 #include "fmha_fwd8w_kernel.h"
+#ifdef XFA_FWD8PP_BODY
+#include XFA_FWD8PP_BODY        // an A/B variant of the generated body
+#else
 #include "fmha_fwd8pp_body.h"
+#endif
 
 namespace xfa {
 
 constexpr int kFwd8ppRows = 256;           // query rows per workgroup (8 waves x 32)
+constexpr int kFwd8ppVReg = kFwd8ppRing * kFwd8wTile;      // the V ring follows the K ring
+constexpr int kFwd8ppSmem = 2 * kFwd8ppRing * kFwd8wTile;  // (kFwd8ppRing: the generated body's)
 
 // One (batch x kv head, 256-row query block) item.
 template <bool F16>
@@ -107,7 +113,7 @@ __device__ __forceinline__ void fwd8pp_item(const FwdParams& p, char* smem, cons
         const int i = lane & 15, q = i >> 1, pb8 = i & 1, g = (lane >> 4) & 1;
         const int r = 4 * hh + (q & 3) + 8 * (q >> 2);   // read kb adds 16 kb rows
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) va[dt] = sbase + kFwd8wVReg + v8w_off(r, 2 * dt + g) + 8 * pb8;
+        for (int dt = 0; dt < 4; ++dt) va[dt] = sbase + kFwd8ppVReg + v8w_off(r, 2 * dt + g) + 8 * pb8;
     }
     const int kstep = __builtin_amdgcn_readfirstlane(kBlockN * k_row);
     const int kdst = __builtin_amdgcn_readfirstlane(sbase + wave * 1024);

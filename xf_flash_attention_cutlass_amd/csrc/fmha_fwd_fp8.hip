@@ -44,9 +44,9 @@ static hipError_t launch_fp8_pp(const FwdParams& p, hipStream_t st) {
         grid = dim3(p.num_cus, 1, 1);
     }
     static std::atomic<unsigned long long> attr_done{0};
-    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8pp_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8wSmem); });
+    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwd8pp_kernel<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwd8ppSmem); });
     note_launch("fmha_fwd8pp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
-    hipLaunchKernelGGL((fmha_fwd8pp_kernel<F16>), grid, dim3(512), kFwd8wSmem, st, pp);
+    hipLaunchKernelGGL((fmha_fwd8pp_kernel<F16>), grid, dim3(512), kFwd8ppSmem, st, pp);
     return hipGetLastError();
 }
 

@@ -28,8 +28,8 @@ namespace xfa {
 
 constexpr int kFwdppRows = 256;            // query rows per workgroup (8 waves x 32)
 constexpr int kFwdppTile = 128 * 64 * 2;   // bytes of one K (or V) tile at D = 128
-constexpr int kFwdppVReg = 4 * kFwdppTile;
-constexpr int kFwdppSmem = 8 * kFwdppTile; // 4 K + 4 V slots, 128 KiB
+constexpr int kFwdppVReg = kFwdppRing * kFwdppTile;      // the V ring follows the K ring
+constexpr int kFwdppSmem = 2 * kFwdppRing * kFwdppTile;  // (kFwdppRing: the generated body's)
 
 __device__ __forceinline__ i32x4 fwdpp_srd(const void* base, uint32_t bytes) {
     const uint64_t a = (uint64_t)base;
@@ -135,6 +135,7 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     // LDS read bases (kv_off image, slot 0; the ring slots are immediate offsets)
     const int sbase = (int)(size_t)smem;
     int kb[2], vb[2];
+    constexpr int kHi = 3 * kFwdppTile;      // the high bases of a 5-slot ring (gen_fwdpp.HI)
     {
         const int q4 = (lane & 15) >> 2;
 #pragma unroll
@@ -151,10 +152,12 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const float thr = __builtin_amdgcn_exp2f(p.max_slack);
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff);
+                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
+                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff);
+                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
+                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
