@@ -68,6 +68,8 @@ DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax
 ALIGN = None           # None: no directive; (a, b): group A's / B's program starts at that offset
                        # mod 8 bytes (.p2align 6, then 4 bytes of s_nop; MI355X_MICROARCH.md,
                        # two waves per SIMD item 8: a hand stream's speed depends on its phase)
+STAMPS = False         # diagnostic build: s_memtime per phase boundary, summed per class in lanes
+                       # 0-7 of %[acc] (fmha_fwdpp_kernel.h XFA_FWDPP_STAMPS; read its SHARES only)
 DMA_IN_M = False       # the DMA pieces ride in the M phase (between MFMAs) instead of the V phase
 RING = 4               # K / V tile slots in LDS
 DLEAD = 3              # V(j) loads tile j + DLEAD (needs RING > DLEAD: B's last read of tile t
@@ -320,6 +322,18 @@ def v_phase(dt, slot, kind, uid, tag):
     return out, stub
 
 
+ST_M, ST_MW, ST_V, ST_VW, ST_PRO, ST_TAIL, ST_EPI = range(7)
+
+
+def st(k):
+    """stamp: the cycles since the previous stamp go to class k (STAMPS builds only)"""
+    if not STAMPS:
+        return []
+    return ["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_sub_u32 s99, s96, s98", "s_mov_b32 s98, s96",
+            f"v_readlane_b32 s97, %[acc], {k}", "s_nop 3", "s_add_u32 s97, s97, s99", "s_nop 3",
+            f"v_writelane_b32 %[acc], s97, {k}"]
+
+
 def m_dma(dt, j_slot, slot, **kw):
     """an M phase (m_phase(dt, j_slot, **kw), or none for j_slot None) carrying the DMA of the
     tile in slot when DMA_IN_M: each piece right after an MFMA, spread over the phase"""
@@ -389,55 +403,56 @@ def group_program(dt, grp):
     if grp:
         out += bar                                          # B runs one phase behind A
     # M(-1) = QK(0) (waves with a visible key), V(-1) = tile-0 max + softmax(0) (masked) + DMA
-    out += [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
-    out += m_dma(dt, RING - 1, DLEAD - 1, pv=False) + m_wait + bar
+    out += st(ST_PRO) + [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
+    out += m_dma(dt, RING - 1, DLEAD - 1, pv=False) + st(ST_M) + m_wait + bar + st(ST_MW)
     v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f")
-    out += first_max() + v + v_wait + bar
+    out += first_max() + v + st(ST_V) + v_wait + bar
     tail += stub
     out += [f"s_branch .Lloop_{uid}", f".Lni_{uid}:"]
     # (no visible key: the same barriers and DMA duty)
-    out += m_dma(dt, None, DLEAD - 1) + m_wait + bar
+    out += m_dma(dt, None, DLEAD - 1) + st(ST_M) + m_wait + bar + st(ST_MW)
     v, _ = v_phase(dt, DLEAD - 1, "n", uid, "fi")
-    out += v + v_wait + bar
+    out += v + st(ST_V) + v_wait + bar
     out += [f".Lloop_{uid}:", f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
             f"s_cbranch_scc1 .Lexit_{uid}"]
     for ph in range(RING):
         vslot = (ph + DLEAD) % RING                          # the tile j+DLEAD this V phase loads
         out.append(f".Lph{ph}_{uid}:")
-        out += [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
+        out += st(ST_VW) + [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         # unmasked step (inline)
-        out += m_dma(dt, ph, vslot) + m_wait + bar
+        out += m_dma(dt, ph, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, stub = v_phase(dt, vslot, "u", uid, f"u{ph}")
-        out += v + v_wait + bar
+        out += v + st(ST_V) + v_wait + bar
         tail += stub
         out += [f".Lnx{ph}_{uid}:", f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
                 f"s_cbranch_scc1 .Lexit_{uid}"]
         # masked step
         tail.append(f".Lm{ph}_{uid}:")
-        tail += m_dma(dt, ph, vslot) + m_wait + bar
+        tail += m_dma(dt, ph, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, stub = v_phase(dt, vslot, "m", uid, f"m{ph}")
-        tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"] + stub
+        tail += v + st(ST_V) + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"] + stub
         # j >= t_w: the last step (PV(j), then the epilogue beside the DMA) or an idle one
         tail += [f".Lx{ph}_{uid}:", f"s_cmp_eq_u32 s{SJ}, %[tw]", f"s_cbranch_scc0 .Li{ph}_{uid}"]
-        tail += m_dma(dt, ph, vslot, qk=False) + m_wait + bar
+        tail += m_dma(dt, ph, vslot, qk=False) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
         # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
-        tail += v + epilogue(dt)
+        tail += v + st(ST_V) + epilogue(dt) + st(ST_EPI)
         tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2) + N_EPI_STORES})"]) + bar
         tail += [f"s_branch .Lnx{ph}_{uid}"]
         tail.append(f".Li{ph}_{uid}:")
-        tail += m_dma(dt, None, vslot) + m_wait + bar
+        tail += m_dma(dt, None, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, _ = v_phase(dt, vslot, "n", uid, f"i{ph}")
-        tail += v + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"]
+        tail += v + st(ST_V) + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
     out.append(f".Lexit_{uid}:")
+    out += st(ST_VW)
     if not grp:
         out += bar                                          # A's closing phase
     # rows that never reached a last step (no visible key): their O = 0, LSE = +inf
     out += [f"s_cmp_eq_u32 s{SST}, 0", f"s_cbranch_scc0 .Ldone_{uid}"] + epilogue(dt)
-    out += [f".Ldone_{uid}:", "s_waitcnt vmcnt(0)", "s_branch .Lend_%="]
+    out += [f".Ldone_{uid}:", "s_waitcnt vmcnt(0)"] + st(ST_TAIL) + ["s_branch .Lend_%="]
     return out + tail + redo_block(dt, uid)
 
 
@@ -446,7 +461,8 @@ def align_head(grp):
 
 
 def item_program(dt):
-    out = ["s_waitcnt lgkmcnt(0)",
+    out = (["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_mov_b32 s98, s96"] if STAMPS else [])
+    out += ["s_waitcnt lgkmcnt(0)",
            f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LIM}, %[lim]",
            f"s_mov_b32 s{SST}, 0"]
     out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
@@ -481,7 +497,7 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
 
 def clobbers():
     regs = [f'"v{i}"' for i in range(96)] + [f'"a{i}"' for i in range(128)]
-    regs += [f'"s{i}"' for i in range(SKR, SCM + 2)]
+    regs += [f'"s{i}"' for i in range(SKR, SCM + 2)] + ([f'"s{i}"' for i in range(96, 100)] if STAMPS else [])
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 
 
@@ -493,6 +509,7 @@ def emit(out=OUT):
         "#pragma once",
         '#include "fmha_common.h"',
         "",
+        *(["#define XFA_FWDPP_STAMPS 1           // diagnostic build (--stamps)"] if STAMPS else []),
         "namespace xfa {",
         "typedef __attribute__((ext_vector_type(4))) int i32x4;",
         f"constexpr int kFwdppRing = {RING};           // K / V tile slots the body addresses",
@@ -502,10 +519,11 @@ def emit(out=OUT):
         prog = item_program(dt)
         prog += GUARDS
         GUARDS.clear()
-        lines.append(f"__device__ __forceinline__ void fwdpp_item_{dt}({SIG}) {{")
+        sig = SIG + (", unsigned& acc" if STAMPS else "")
+        lines.append(f"__device__ __forceinline__ void fwdpp_item_{dt}({sig}) {{")
         lines.append("    asm volatile(")
         lines += [f'        "{b}\\n"' for b in prog]
-        lines.append("        :")
+        lines.append('        : [acc] "+v"(acc)' if STAMPS else "        :")
         hi = ['[kh0] "v"(kh0)', '[kh1] "v"(kh1)', '[vh0] "v"(vh0)', '[vh1] "v"(vh1)'] if RING > 4 else []
         lines.append("        : " + ",\n          ".join(OPS + hi))
         lines.append(f"        : {clobbers()});")
@@ -525,11 +543,13 @@ if __name__ == "__main__":
     ap.add_argument("--ring", type=int, default=RING, help="K / V tile slots in LDS")
     ap.add_argument("--dlead", type=int, default=DLEAD, help="V(j) loads tile j + dlead")
     ap.add_argument("--dma-in-m", action="store_true", help="DMA pieces in the MFMA phase")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic phase stamps (XFA_FWDPP_STAMPS)")
     ap.add_argument("--align", default=None, help="A,B: the groups' program starts mod 8 (0 or 4)")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     LEAD, DMAMIX, RING, DLEAD, DMA_IN_M = a.lead, a.dmamix, a.ring, a.dlead, a.dma_in_m
     ALIGN = None if a.align is None else tuple(int(x) for x in a.align.split(","))
+    STAMPS = a.stamps
     assert 3 <= DLEAD < RING <= 5
     ABL = set(x for x in a.abl.split(",") if x)
     emit(a.out)

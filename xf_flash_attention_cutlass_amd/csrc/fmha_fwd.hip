@@ -211,3 +211,16 @@ hipError_t XFA_FN(XFA_HD, XFA_DTN)(const FwdParams& p, hipStream_t st) {
 }
 
 }  // namespace xfa
+
+#if defined(XFA_FWDPP_STAMPS) && XFA_HD == 128 && XFA_DT_BF16
+// diagnostic builds only: copy out (and optionally clear) the ping-pong phase stamps
+extern "C" int fmha_fwdpp_stamps(unsigned* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(xfa::g_fwdpp_stamps), sizeof(xfa::g_fwdpp_stamps)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned zero[8 * 8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(xfa::g_fwdpp_stamps), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -27,6 +27,18 @@
 namespace xfa {
 
 constexpr int kFwdppRows = 256;            // query rows per workgroup (8 waves x 32)
+
+#ifdef XFA_FWDPP_STAMPS
+// Diagnostic build only (tools/fwdpp_variants.sh "name=--stamps", tools/pp_stamps.py): each wave
+// sums the s_memtime cycles of every phase class (gen_fwdpp.ST_*) over its items in lanes 0-7 of
+// one register; the kernel adds them into this array at its end (read by fmha_fwdpp_stamps).
+static __device__ unsigned g_fwdpp_stamps[8 * 8];
+#define XFA_PP_ACC_PARAM , unsigned& acc
+#define XFA_PP_ACC_ARG , acc
+#else
+#define XFA_PP_ACC_PARAM
+#define XFA_PP_ACC_ARG
+#endif
 constexpr int kFwdppTile = 128 * 64 * 2;   // bytes of one K (or V) tile at D = 128
 constexpr int kFwdppVReg = kFwdppRing * kFwdppTile;      // the V ring follows the K ring
 constexpr int kFwdppSmem = 2 * kFwdppRing * kFwdppTile;  // (kFwdppRing: the generated body's)
@@ -43,7 +55,7 @@ __device__ __forceinline__ i32x4 fwdpp_srd(const void* base, uint32_t bytes) {
 
 // One (batch x kv head, 256-row query block) item.
 template <bool BF16>
-__device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const int bh, const int m_block) {
+__device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const int bh, const int m_block XFA_PP_ACC_PARAM) {
     constexpr int HD = 128;
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));       // item-local: not hoisted out of the persistent loop
@@ -153,11 +165,11 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi);
+                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi);
+                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
@@ -168,6 +180,9 @@ __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
     __shared__ int s_claim[2];
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
+#ifdef XFA_FWDPP_STAMPS
+    unsigned acc = 0;
+#endif
     for (int k = 0;; ++k) {
         int bh, m_block;
         if (p.persistent == 2) {
@@ -204,8 +219,11 @@ __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
-        fwdpp_item<BF16>(p, smem, bh, m_block);
+        fwdpp_item<BF16>(p, smem, bh, m_block XFA_PP_ACC_ARG);
     }
+#ifdef XFA_FWDPP_STAMPS
+    if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwdpp_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], acc);
+#endif
     if (p.persistent == 3 && threadIdx.x == 0) {
         const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
         if (atomicAdd(p.work_ctr + 1, 1) == total - 1) {
