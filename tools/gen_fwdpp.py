@@ -57,7 +57,7 @@ LT, NM, LRUN, LIM, MISC = 56, 57, 58, 59, 60
 ABASE_O, ABASE_Q, ABASE_K, VBASE_V = 0, 64, 96, 64
 SKR, SVR = 80, 84
 SJ, ST, SST, SRA, SCM = 88, 89, 90, 92, 94
-ABL = set()            # timing ablations (results INVALID): nosm noredo nopro; noepiwait (valid)
+ABL = set()            # timing ablations (results INVALID): nosm noredo nopro nopq nopkv; noepiwait (valid)
 # (tools/gen_fwd8pp.py reuses this generator's phase program for the fp8 kernel: it rebinds the
 #  operand-specific functions below and these parameters)
 XDL_NOPS = ["s_nop 7", "s_nop 7", "s_nop 3"]   # last MFMA write -> VALU read of O / S
@@ -466,16 +466,17 @@ def item_program(dt):
     out += ["s_waitcnt lgkmcnt(0)",
            f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LIM}, %[lim]",
            f"s_mov_b32 s{SST}, 0"]
-    if "nopro" not in ABL:
+    if not ABL & {"nopro", "nopq"}:
         out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
     out += [f"v_accvgpr_write_b32 a{ABASE_O + i}, 0" for i in range(64)]
     for r, lo, hi in ((SKR, "kblo", "kbhi"), (SVR, "vblo", "vbhi")):
         out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
                 f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
     for slot in range(DLEAD - 1):                            # tiles 0 .. DLEAD-2
-        out += ([] if "nopro" in ABL else sum(dma_pieces(slot), [])) + dma_advance()
+        out += ([] if ABL & {"nopro", "nopkv"} else sum(dma_pieces(slot), [])) + dma_advance()
     # Q and tile 0 landed, published
-    out += ([] if "nopro" in ABL else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2)})"]) + ["s_barrier"]
+    w = NPIECE * (DLEAD - 2) if not ABL & {"nopro", "nopkv"} else 0
+    out += ([] if "nopro" in ABL else [f"s_waitcnt vmcnt({w})"]) + ["s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
     out += align_head(0) + group_program(dt, 0) + align_head(1)[:1] + [".LgrpB_%=:"]
     out += align_head(1)[1:] + group_program(dt, 1) + [".Lend_%=:"]
