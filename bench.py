@@ -498,6 +498,8 @@ class ClockMonitor:
             except (OSError, subprocess.SubprocessError):
                 self.proc.kill()
             self.proc = None
+        import shutil
+        shutil.rmtree(os.path.dirname(self.path), ignore_errors=True)
 
 
 MONITOR = None
