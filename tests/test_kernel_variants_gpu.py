@@ -1,0 +1,68 @@
+"""GPU: the generated D = 128 forward kernels the knobs select, in the default run.
+
+fwd_w4 = 1 (4-wave, csrc/fmha_fwd4_kernel.h) and 2 (8-wave ping-pong, csrc/fmha_fwdpp_kernel.h,
+the default); fp8_w4 = 1 (4-wave fp8, the default) and 2 (ping-pong fp8,
+csrc/fmha_fwd8pp_kernel.h).  Each setting runs the same cases: the kernel id is asserted
+(fmha_last_kernel), the output is held to the oracle by the reference's rule (test.py:975), and
+the two kernels of a pair must agree bit for bit - they compute every row with the same tile
+order, reference max and operation order, only the row-to-wave split and the schedule differ.
+(The whole GPU suite also runs under each non-default value: profiles/r05_knob_suite.log.)
+"""
+import pytest
+import torch
+
+from oracle import attention_ref as orc
+from tests import test_fp8_gpu as f8
+from tests import test_fwd4_redo_gpu as r4
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def xfa():
+    import xf_flash_attention_cutlass_amd as m
+    return m
+
+
+BF16_CASES = [
+    # b, h, hk, sq, sk, causal, window
+    (2, 4, 4, 700, 700, True, (-1, -1)),
+    (1, 8, 2, 513, 1025, False, (-1, -1)),
+    (2, 4, 4, 300, 900, True, (-1, -1)),
+    (1, 4, 4, 1024, 1024, False, (-1, 200)),    # right window only (a left one: 8-wave kernel)
+]
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal,window", BF16_CASES)
+def test_fwd_w4_kernels_agree(b, h, hk, sq, sk, causal, window):
+    g = torch.Generator().manual_seed(sq + sk)
+    q = torch.randn(b, sq, h, 128, generator=g).bfloat16()
+    k = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
+    v = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
+    outs = {}
+    for w4 in (1, 2):
+        with r4._option("fwd_w4", w4):
+            outs[w4] = r4._fwd(q, k, v, causal, window)     # asserts the kernel id for w4
+    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
+    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
+    ok, err, bound = orc.parity_ok(outs[2][0].float(), ref, pt, 2.0, 0.0)
+    assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
+    assert torch.equal(outs[1][0], outs[2][0])
+    assert torch.equal(outs[1][1], outs[2][1])
+
+
+FP8_CASES = [
+    # b, h, hk, sq, sk, causal
+    (2, 4, 2, 700, 700, True),
+    (1, 8, 8, 513, 1025, False),
+    (2, 4, 4, 300, 900, True),
+]
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal", FP8_CASES)
+def test_fp8_w4_kernels_agree(xfa, b, h, hk, sq, sk, causal):
+    outs = {}
+    for w4 in (1, 2):
+        with r4._option("fp8_w4", w4):
+            outs[w4] = f8._check(xfa, b, h, hk, sq, sk, causal=causal, seed=sq)  # oracle + kernel id
+    assert torch.equal(outs[1], outs[2])
