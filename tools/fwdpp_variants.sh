@@ -3,8 +3,8 @@
 # variants/fwdpp_NAME.h with `tools/gen_fwdpp.py ARGS` and links variants/lib_NAME.so with the two
 # hd128 forward objects rebuilt against it; compare with tools/lib_ab.py (path@fwd_w4=2).
 # With --fp8 first, the fp8 body (tools/gen_fwd8pp.py -> the fwd_fp8 object; path@fp8_w4=2).
-#   tools/fwdpp_variants.sh "nomix=--no-dmamix" ...
-#   tools/fwdpp_variants.sh --fp8 "r5l4=--ring 5 --dlead 4" ...
+#   tools/fwdpp_variants.sh "nosm=--abl nosm" "st=--stamps" ...
+#   tools/fwdpp_variants.sh --fp8 "nosm=--abl nosm" ...
 set -e
 cd "$(dirname "$0")/.."
 gen=tools/gen_fwdpp.py; def=XFA_FWDPP_BODY; objs="fwd:128:bf16 fwd:128:f16"

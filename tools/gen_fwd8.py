@@ -398,12 +398,8 @@ def redo_block(par, uid):
     return out
 
 
-ALIGN = None           # None: no directive; 0 / 4: the body starts at that offset mod 8 bytes
-
-
 def item_program(dt, uid="%="):
-    out = ([] if ALIGN is None else [".p2align 6"] + ["s_nop 0"] * (ALIGN // 4))
-    out += ["s_waitcnt lgkmcnt(0)"]
+    out = ["s_waitcnt lgkmcnt(0)"]
     out += [f"v_mov_b32 v{PINF}, 0x7f800000", f"v_mov_b32 v{NINF}, 0xff800000",
             f"v_mov_b32 v{SC127}, 0x7f",
             f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{NM + 1}, 0",
@@ -624,10 +620,8 @@ if __name__ == "__main__":
     ap.add_argument("--no-lead2", dest="lead2", action="store_false",
                     help="DMA two steps ahead only (3 V^T fragments prefetched)")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
-    ap.add_argument("--align", type=int, choices=[0, 4], default=None, help="body start mod 8")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
-    ALIGN = a.align
     ABL = set(x for x in a.abl.split(",") if x)
     QK_LEAD = a.qklead
     LEAD2 = a.lead2

@@ -184,8 +184,7 @@ def item_program(dt):
     # Q and tile 0 landed, published
     out += [f"s_waitcnt vmcnt({pp.NPIECE * (pp.DLEAD - 2)})", "s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
-    out += pp.align_head(0) + pp.group_program(dt, 0) + pp.align_head(1)[:1] + [".LgrpB_%=:"]
-    out += pp.align_head(1)[1:] + pp.group_program(dt, 1) + [".Lend_%=:"]
+    out += pp.group_program(dt, 0) + [".LgrpB_%=:"] + pp.group_program(dt, 1) + [".Lend_%=:"]
     return out
 
 
@@ -240,16 +239,7 @@ if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
-    ap.add_argument("--no-dmamix", dest="dmamix", action="store_false")
-    ap.add_argument("--ring", type=int, default=pp.RING, help="K / V tile slots in LDS")
-    ap.add_argument("--dlead", type=int, default=pp.DLEAD, help="V(j) loads tile j + dlead")
-    ap.add_argument("--dma-in-m", action="store_true", help="DMA pieces in the MFMA phase")
-    ap.add_argument("--align", default=None, help="A,B: the groups' program starts mod 8 (0 or 4)")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
-    pp.ALIGN = None if a.align is None else tuple(int(x) for x in a.align.split(","))
-    pp.RING, pp.DLEAD, pp.DMA_IN_M = a.ring, a.dlead, a.dma_in_m
-    assert 3 <= pp.DLEAD < pp.RING
     pp.ABL = set(x for x in a.abl.split(",") if x)
-    pp.DMAMIX = a.dmamix
     emit(a.out)

@@ -65,12 +65,8 @@ VPH_NOPS = ["s_nop 7", "s_nop 7"]              # (a V phase: after its first DMA
 NPIECE = 4             # LDS-DMA pieces per wave per tile (A's publish wait keeps them in flight)
 EPI_SCALE = None       # an SGPR operand O is also scaled by in the epilogue (fp8: %[vsc])
 DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax (else all first)
-ALIGN = None           # None: no directive; (a, b): group A's / B's program starts at that offset
-                       # mod 8 bytes (.p2align 6, then 4 bytes of s_nop; MI355X_MICROARCH.md,
-                       # two waves per SIMD item 8: a hand stream's speed depends on its phase)
 STAMPS = False         # diagnostic build: s_memtime per phase boundary, summed per class in lanes
                        # 0-7 of %[acc] (fmha_fwdpp_kernel.h XFA_FWDPP_STAMPS; read its SHARES only)
-DMA_IN_M = False       # the DMA pieces ride in the M phase (between MFMAs) instead of the V phase
 RING = 4               # K / V tile slots in LDS
 DLEAD = 3              # V(j) loads tile j + DLEAD (needs RING > DLEAD: B's last read of tile t
                        # is in global phase 2t+3, A's load of tile t+RING in 2(t+RING-DLEAD)+3)
@@ -117,29 +113,15 @@ def value_info(v):
     return off, ks * 4 + ((r & 7) >> 1)
 
 
-HI = 3                 # with RING > 4, slots >= HI address from the high bases (kh, vh = base +
-                       # HI tiles): a ds_read offset holds 16 bits
-
-
-def lds_base(name, slot_tile):
-    if RING > 4 and slot_tile >= HI:
-        return f"%[{name[0]}h{name[-1]}]", (slot_tile - HI) * TILE
-    return f"%[{name}]", slot_tile * TILE
-
-
 def k_read(f, slot_tile, dst_slot):
     s, kt = f // 2, f % 2
-    b, o = lds_base(f"kb{s & 1}", slot_tile)
-    return f"ds_read_b128 {ktup(dst_slot)}, {b} offset:{o + kt * 4 * RB + 512 * (s >> 1)}"
+    return f"ds_read_b128 {ktup(dst_slot)}, %[kb{s & 1}] offset:{slot_tile * TILE + kt * 4 * RB + 512 * (s >> 1)}"
 
 
 def v_reads(f, slot_tile, dst_slot):
     ks, d = f // 4, f % 4
-    out = []
-    for h in (0, 1):
-        b, o = lds_base(f"vb{h}", slot_tile)                # (the lane base carries the V ring)
-        out.append(f"ds_read_b64_tr_b16 {vtup(dst_slot, h)}, {b} offset:{o + 2 * ks * RB + 512 * d}")
-    return out
+    off = slot_tile * TILE + 2 * ks * RB + 512 * d          # (the lane base carries the V ring)
+    return [f"ds_read_b64_tr_b16 {vtup(dst_slot, h)}, %[vb{h}] offset:{off}" for h in (0, 1)]
 
 
 def m_phase(dt, j_slot, pv=True, qk=True):
@@ -303,11 +285,11 @@ def redo_check(uid, tag):
 def v_phase(dt, slot, kind, uid, tag):
     """V phase: kind 'u' unmasked softmax, 'm' masked, 'n' none; DMA of the tile in slot.
     Returns (inline, out-of-line stubs)."""
-    pieces = [] if DMA_IN_M else dma_pieces(slot)
+    pieces = dma_pieces(slot)
     if kind == "n" or ("nosm" in ABL and kind == "u"):
         return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
     sm = softmax(dt, kind == "m")
-    if DMAMIX and pieces:
+    if DMAMIX:
         out = pieces[0] + VPH_NOPS                      # last QK^T results -> VALU
         # the other pieces spread through the softmax
         step = len(sm) // len(pieces)
@@ -332,23 +314,6 @@ def st(k):
     return ["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_sub_u32 s99, s96, s98", "s_mov_b32 s98, s96",
             f"v_readlane_b32 s97, %[acc], {k}", "s_nop 3", "s_add_u32 s97, s97, s99", "s_nop 3",
             f"v_writelane_b32 %[acc], s97, {k}"]
-
-
-def m_dma(dt, j_slot, slot, **kw):
-    """an M phase (m_phase(dt, j_slot, **kw), or none for j_slot None) carrying the DMA of the
-    tile in slot when DMA_IN_M: each piece right after an MFMA, spread over the phase"""
-    out = [] if j_slot is None else m_phase(dt, j_slot, **kw)
-    if not DMA_IN_M:
-        return out
-    pieces = dma_pieces(slot)
-    at = [i for i, x in enumerate(out) if x.startswith("v_mfma")]
-    if not at:
-        return sum(pieces, []) + out
-    n = len(pieces)
-    for k in reversed(range(n)):
-        i = at[(k * len(at)) // n] + 1
-        out[i:i] = pieces[k]
-    return out
 
 
 def epilogue_core(dt):
@@ -396,7 +361,7 @@ def group_program(dt, grp):
     uid = f"{'AB'[grp]}_%="
     # tile t is published at the barrier closing global phase 2t-1: A (after V(t-2)) has loaded
     # through tile t-2+DLEAD, B (after M(t-2), its loads one phase later) through t-3+DLEAD
-    m_wait = [f"s_waitcnt vmcnt({NPIECE * (DLEAD - (2 if DMA_IN_M else 3))})"] if grp else []
+    m_wait = [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 3)})"] if grp else []
     v_wait = [] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2)})"]
     bar = ["s_barrier"]
     out, tail = [], []
@@ -404,13 +369,13 @@ def group_program(dt, grp):
         out += bar                                          # B runs one phase behind A
     # M(-1) = QK(0) (waves with a visible key), V(-1) = tile-0 max + softmax(0) (masked) + DMA
     out += st(ST_PRO) + [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
-    out += m_dma(dt, RING - 1, DLEAD - 1, pv=False) + st(ST_M) + m_wait + bar + st(ST_MW)
+    out += m_phase(dt, RING - 1, pv=False) + st(ST_M) + m_wait + bar + st(ST_MW)
     v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f")
     out += first_max() + v + st(ST_V) + v_wait + bar
     tail += stub
     out += [f"s_branch .Lloop_{uid}", f".Lni_{uid}:"]
     # (no visible key: the same barriers and DMA duty)
-    out += m_dma(dt, None, DLEAD - 1) + st(ST_M) + m_wait + bar + st(ST_MW)
+    out += st(ST_M) + m_wait + bar + st(ST_MW)
     v, _ = v_phase(dt, DLEAD - 1, "n", uid, "fi")
     out += v + st(ST_V) + v_wait + bar
     out += [f".Lloop_{uid}:", f"s_mov_b32 s{SJ}, 0", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
@@ -422,7 +387,7 @@ def group_program(dt, grp):
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         # unmasked step (inline)
-        out += m_dma(dt, ph, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
+        out += m_phase(dt, ph) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, stub = v_phase(dt, vslot, "u", uid, f"u{ph}")
         out += v + st(ST_V) + v_wait + bar
         tail += stub
@@ -430,19 +395,19 @@ def group_program(dt, grp):
                 f"s_cbranch_scc1 .Lexit_{uid}"]
         # masked step
         tail.append(f".Lm{ph}_{uid}:")
-        tail += m_dma(dt, ph, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
+        tail += m_phase(dt, ph) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, stub = v_phase(dt, vslot, "m", uid, f"m{ph}")
         tail += v + st(ST_V) + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"] + stub
         # j >= t_w: the last step (PV(j), then the epilogue beside the DMA) or an idle one
         tail += [f".Lx{ph}_{uid}:", f"s_cmp_eq_u32 s{SJ}, %[tw]", f"s_cbranch_scc0 .Li{ph}_{uid}"]
-        tail += m_dma(dt, ph, vslot, qk=False) + st(ST_M) + m_wait + bar + st(ST_MW)
+        tail += m_phase(dt, ph, qk=False) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
         # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
         tail += v + st(ST_V) + epilogue(dt) + st(ST_EPI)
         tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2) + N_EPI_STORES})"]) + bar
         tail += [f"s_branch .Lnx{ph}_{uid}"]
         tail.append(f".Li{ph}_{uid}:")
-        tail += m_dma(dt, None, vslot) + st(ST_M) + m_wait + bar + st(ST_MW)
+        tail += st(ST_M) + m_wait + bar + st(ST_MW)
         v, _ = v_phase(dt, vslot, "n", uid, f"i{ph}")
         tail += v + st(ST_V) + v_wait + bar + [f"s_branch .Lnx{ph}_{uid}"]
     out.append(f"s_branch .Lph0_{uid}")
@@ -455,10 +420,6 @@ def group_program(dt, grp):
     out += [f".Ldone_{uid}:"] + ([] if "noepiwait" in ABL else ["s_waitcnt vmcnt(0)"])
     out += st(ST_TAIL) + ["s_branch .Lend_%="]
     return out + tail + redo_block(dt, uid)
-
-
-def align_head(grp):
-    return [] if ALIGN is None else [".p2align 6"] + ["s_nop 0"] * (ALIGN[grp] // 4)
 
 
 def item_program(dt):
@@ -478,8 +439,7 @@ def item_program(dt):
     w = NPIECE * (DLEAD - 2) if not ABL & {"nopro", "nopkv"} else 0
     out += ([] if "nopro" in ABL else [f"s_waitcnt vmcnt({w})"]) + ["s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
-    out += align_head(0) + group_program(dt, 0) + align_head(1)[:1] + [".LgrpB_%=:"]
-    out += align_head(1)[1:] + group_program(dt, 1) + [".Lend_%=:"]
+    out += group_program(dt, 0) + [".LgrpB_%=:"] + group_program(dt, 1) + [".Lend_%=:"]
     return out
 
 
@@ -487,8 +447,7 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const i32x4 qsrd, const i32x4 osrd, const i32x4 lsrd, const int kstep, const int kdst, "
        "const int ntl, const int tw, const int ew, const int grp, const float c, const float thr, "
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
-       "const int lim, const int qoff, const int ooff, const int loff, "
-       "const int kh0, const int kh1, const int vh0, const int vh1")
+       "const int lim, const int qoff, const int ooff, const int loff")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
@@ -527,8 +486,7 @@ def emit(out=OUT):
         lines.append("    asm volatile(")
         lines += [f'        "{b}\\n"' for b in prog]
         lines.append('        : [acc] "+v"(acc)' if STAMPS else "        :")
-        hi = ['[kh0] "v"(kh0)', '[kh1] "v"(kh1)', '[vh0] "v"(vh0)', '[vh1] "v"(vh1)'] if RING > 4 else []
-        lines.append("        : " + ",\n          ".join(OPS + hi))
+        lines.append("        : " + ",\n          ".join(OPS))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
         lines.append("")
@@ -540,19 +498,10 @@ def emit(out=OUT):
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lead", type=int, default=LEAD, help="gaps an LDS read leads its MFMA")
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
-    ap.add_argument("--no-dmamix", dest="dmamix", action="store_false")
-    ap.add_argument("--ring", type=int, default=RING, help="K / V tile slots in LDS")
-    ap.add_argument("--dlead", type=int, default=DLEAD, help="V(j) loads tile j + dlead")
-    ap.add_argument("--dma-in-m", action="store_true", help="DMA pieces in the MFMA phase")
     ap.add_argument("--stamps", action="store_true", help="diagnostic phase stamps (XFA_FWDPP_STAMPS)")
-    ap.add_argument("--align", default=None, help="A,B: the groups' program starts mod 8 (0 or 4)")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
-    LEAD, DMAMIX, RING, DLEAD, DMA_IN_M = a.lead, a.dmamix, a.ring, a.dlead, a.dma_in_m
-    ALIGN = None if a.align is None else tuple(int(x) for x in a.align.split(","))
-    STAMPS = a.stamps
-    assert 3 <= DLEAD < RING <= 5
     ABL = set(x for x in a.abl.split(",") if x)
+    STAMPS = a.stamps
     emit(a.out)

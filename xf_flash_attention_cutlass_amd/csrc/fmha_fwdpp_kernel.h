@@ -147,7 +147,6 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     // LDS read bases (kv_off image, slot 0; the ring slots are immediate offsets)
     const int sbase = (int)(size_t)smem;
     int kb[2], vb[2];
-    constexpr int kHi = 3 * kFwdppTile;      // the high bases of a 5-slot ring (gen_fwdpp.HI)
     {
         const int q4 = (lane & 15) >> 2;
 #pragma unroll
@@ -164,12 +163,10 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const float thr = __builtin_amdgcn_exp2f(p.max_slack);
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi XFA_PP_ACC_ARG);
+                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        kb[0] + kHi, kb[1] + kHi, vb[0] + kHi, vb[1] + kHi XFA_PP_ACC_ARG);
+                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
