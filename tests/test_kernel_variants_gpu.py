@@ -66,3 +66,42 @@ def test_fp8_w4_kernels_agree(xfa, b, h, hk, sq, sk, causal):
         with r4._option("fp8_w4", w4):
             outs[w4] = f8._check(xfa, b, h, hk, sq, sk, causal=causal, seed=sq)  # oracle + kernel id
     assert torch.equal(outs[1], outs[2])
+
+
+def _sweep(n, seed):
+    """seeded random shapes around the edges the kernels special-case: lengths below one key
+    tile, at and just past 64 / 256 multiples, sq > sk (rows with no key under causal), GQA
+    groups 1-8, right windows, fp16"""
+    g = torch.Generator().manual_seed(seed)
+    lens = [1, 17, 63, 64, 65, 255, 256, 257, 383, 512, 777]
+    out = []
+    for _ in range(n):
+        pick = lambda xs: xs[int(torch.randint(len(xs), (1,), generator=g))]  # noqa: E731
+        hk = pick([1, 2, 4])
+        grp = pick([1, 2, 4, 8]) if hk < 4 else pick([1, 2])
+        mode = pick(["causal", "none", "right"])
+        window = (-1, pick([0, 5, 100])) if mode == "right" else (-1, -1)
+        sq = pick(lens)
+        if sq * grp <= 32:        # a whole GQA group in one 32-row tile: the decode kernel's
+            continue
+        out.append((pick([1, 2]), hk * grp, hk, sq, pick(lens), mode == "causal", window,
+                    pick([torch.bfloat16, torch.float16])))
+    return out
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal,window,dt", _sweep(20, 5))
+def test_fwd_w4_kernels_sweep(b, h, hk, sq, sk, causal, window, dt):
+    g = torch.Generator().manual_seed(b * 1000 + sq * 7 + sk)
+    q = torch.randn(b, sq, h, 128, generator=g).to(dt)
+    k = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    v = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    outs = {}
+    for w4 in (1, 2):
+        with r4._option("fwd_w4", w4):
+            outs[w4] = r4._fwd(q, k, v, causal, window)
+    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
+    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
+    ok, err, bound = orc.parity_ok(outs[2][0].float(), ref, pt, 2.0, 1e-5)
+    assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
+    assert torch.equal(outs[1][0], outs[2][0])
+    assert torch.equal(outs[1][1], outs[2][1])
