@@ -105,3 +105,23 @@ def test_fwd_w4_kernels_sweep(b, h, hk, sq, sk, causal, window, dt):
     assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
     assert torch.equal(outs[1][0], outs[2][0])
     assert torch.equal(outs[1][1], outs[2][1])
+
+
+def _sweep8(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    lens = [17, 64, 65, 255, 256, 257, 511, 777]
+    out = []
+    for _ in range(n):
+        pick = lambda xs: xs[int(torch.randint(len(xs), (1,), generator=g))]  # noqa: E731
+        hk = pick([1, 2, 4])
+        out.append((pick([1, 2]), hk * pick([1, 2, 4]), hk, pick(lens), pick(lens), bool(pick([0, 1]))))
+    return out
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal", _sweep8(10, 11))
+def test_fp8_w4_kernels_sweep(xfa, b, h, hk, sq, sk, causal):
+    outs = {}
+    for w4 in (1, 2):
+        with r4._option("fp8_w4", w4):
+            outs[w4] = f8._check(xfa, b, h, hk, sq, sk, causal=causal, seed=sk)
+    assert torch.equal(outs[1], outs[2])
