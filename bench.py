@@ -470,6 +470,17 @@ class ClockMonitor:
         except OSError:
             self.proc = None
 
+    def select(self, pci_bus):
+        """Point the sampler at this process' device (amd-smi numbers all of the machine's
+        GPUs, whatever HIP_VISIBLE_DEVICES says)."""
+        self.bdf = pci_bus.lower()
+        if self.proc:
+            try:
+                self.proc.stdin.write(f"bdf {self.bdf}\n".encode())
+                self.proc.stdin.flush()
+            except OSError:
+                pass
+
     def samples(self):
         try:
             with open(self.path) as f:
@@ -479,6 +490,12 @@ class ClockMonitor:
 
     def stats(self, t0, t1):
         ss = [x for x in self.samples() if t0 <= x["t"] <= t1 and x.get("gfx_mhz")]
+        want = getattr(self, "bdf", None)
+        mine = [x for x in ss if want and str(x.get("bdf") or "").startswith(want)]
+        # samples of this process' own GPU when amd-smi matched its BDF; otherwise amd-smi's
+        # GPU 0, flagged as possibly another GPU of the machine
+        matched = bool(mine)
+        ss = mine or ss
         if not ss:
             return {"samples": 0, "source": "amd-smi metric (no samples in the window)"}
         per = sorted(sum(x["gfx_mhz"]) / len(x["gfx_mhz"]) for x in ss)   # mean over XCDs
@@ -488,6 +505,7 @@ class ClockMonitor:
                 "gfx_mhz_median": round(med(per), 1), "gfx_mhz_min": round(per[0], 1),
                 "gfx_mhz_max": round(per[-1], 1),
                 "power_w_median": med(pw), "power_w_max": pw[-1] if pw else None,
+                "bdf": ss[-1].get("bdf"), "bdf_match": matched,
                 "source": "amd-smi metric -c -p (current gfx clock, mean over XCDs; socket power)"}
 
     def close(self):
@@ -666,10 +684,13 @@ def main(argv=None):
 def run(a, world, rank, local):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if MONITOR:
+        MONITOR.select(device_info(dev)["pci_bus"])   # sample this rank's own GPU
     dist = None
     if world > 1 or "WORLD_SIZE" in os.environ:
-        # (a one-rank group too when launched by torch.distributed.run: the sharded path and
-        # its RCCL all-gather then run and are timed exactly as at N > 1)
+        # (a one-rank group too when launched by torch.distributed.run: the sharded path runs
+        # as at N > 1, but at world size 1 no collective is issued — all_gather_dim returns the
+        # local shard — so the all-gather line then times nothing)
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     _set_options(a.opt)

@@ -98,7 +98,8 @@ const char* fmha_last_error(void);
 int fmha_last_status(void);
 
 /* KV split count the last forward call on this thread launched with (1 = single pass; decode
- * kernel: one split per wave).  Diagnostic, for tests and tuning. */
+ * kernel: one split per wave; 0 if that call launched nothing).  Diagnostic, for tests and
+ * tuning. */
 int fmha_last_num_splits(void);
 
 /* The forward kernel the last forward call on this thread launched, with its schedule, e.g.
@@ -236,11 +237,15 @@ void fmha_kvcache_append(void* q, void* q_out, void* kcache, void* vcache, const
  * dk/dv [b,sk,hk,d] (GQA groups reduced in-kernel, no host sum_out), softmax_d fp32
  * [batch, heads, seqlen_q] (may be NULL: then pool scratch is used).  p_dropout: the forward's,
  * with the same fmha_set_rng_state (the keep bits are regenerated, not stored).
- * deterministic: dQ partials of each key block go to their own fp32 slice and are summed in
- * key-block order (bitwise reproducible; export.cpp:1086-1092 splits dq_accum the same way),
- * instead of float atomics into one accumulator.
+ * deterministic: S = min(ceil(CUs / (b * hk)), key blocks) fp32 dQ slices (the bound of
+ * export.cpp:1086-1092), each owned by one workgroup that walks its key blocks in a fixed order
+ * and adds by plain read-modify-write (D <= 128; D > 128: float atomics into the slice), then
+ * summed in slice order: bitwise reproducible for a given S, instead of float atomics into one
+ * accumulator.  S also stops at 1 + 8 GiB / (one slice's bytes).
  * workspace: optional caller scratch of fmha_bwd_workspace_size(..., deterministic) bytes;
- * NULL = pool.  One sequence's slab of any tensor must stay under 2 GiB - 256 bytes (32-bit
+ * NULL = pool.  A shorter workspace (at least one slice) is accepted and runs with as many
+ * slices as it holds: still reproducible, but the dQ bits then depend on that slice count, so
+ * pass the full size when results must match across callers.  One sequence's slab of any tensor must stay under 2 GiB - 256 bytes (32-bit
  * buffer offsets); larger inputs fail with an error, never a wrong result. */
 void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_lse,
               void* dq, void* dk, void* dv, void* alibi_slopes, void* softmax_d,

@@ -156,6 +156,95 @@ def _worker(rank, world, port, kind, q):
         dist.destroy_process_group()
 
 
+def _grad_worker(rank, world, port, kind, q):
+    """Backward through the sharded paths: every rank computes the same loss from the gathered
+    output; the all-gathers' backward narrows the gradient to the rank's shard, so the ranks'
+    gradients of the replicated q / k / v, summed, are the unsharded gradients."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import attention_ref as orc
+        torch.manual_seed(0)
+        if kind == "varlen":
+            lens = [5, 17, 1, 30, 9]
+            n = sum(lens)
+            x, k, v = torch.randn(n, 4, 16), torch.randn(n, 2, 16), torch.randn(n, 2, 16)
+
+            def local(qq, kk, vv, cq, ck, mq, mk, causal=False):
+                outs = []
+                for i in range(len(cq) - 1):
+                    a, b = int(cq[i]), int(cq[i + 1])
+                    c, d = int(ck[i]), int(ck[i + 1])
+                    outs.append(orc.attention_ref(qq[a:b][None], kk[c:d][None], vv[c:d][None],
+                                                  causal=causal)[0][0])
+                return torch.cat(outs)
+            plan = sh.varlen_plan(lens, lens, world, rank, "cpu")   # host lengths: no sync
+            cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
+
+            def run(a, b, c, sharded):
+                if sharded:
+                    return sh.sharded_varlen(a, b, c, local_fn=local, plan=plan, causal=True)[0]
+                return local(a, b, c, cu, cu, max(lens), max(lens), causal=True)
+        else:
+            shapes = {"heads": ((2, 24, 8, 16), 4), "heads_uneven": ((2, 20, 6, 16), 3),
+                      "batch": ((3, 20, 2, 16), 1)}
+            (b, s_, h, d), hk = shapes[kind]
+            x, k, v = torch.randn(b, s_, h, d), torch.randn(b, s_, hk, d), torch.randn(b, s_, hk, d)
+
+            def local(qq, kk, vv, causal=False):
+                return orc.attention_ref(qq, kk, vv, causal=causal)[0]
+
+            def run(a, b_, c, sharded):
+                if sharded:
+                    return sh.sharded_attention(a, b_, c, local_fn=local, causal=True)[0]
+                return local(a, b_, c, causal=True)
+        w = torch.randn(x.shape[:-1] + (v.shape[-1],))
+        grads = []
+        for sharded in (True, False):
+            xs, ks, vs = (t.clone().requires_grad_(True) for t in (x, k, v))
+            out = run(xs, ks, vs, sharded)
+            (out * w).sum().backward()
+            grads.append([t.grad for t in (xs, ks, vs)])
+        ok = True
+        for gs, gr in zip(*grads):
+            dist.all_reduce(gs)          # each rank holds its shard's part; the sum is the whole
+            ok = ok and torch.allclose(gs, gr, atol=1e-5)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    return dict(q.get(timeout=5) for _ in range(2))
+
+
+@pytest.mark.parametrize("kind", ["heads", "heads_uneven", "batch", "varlen"])
+def test_sharded_backward_world2_gloo(kind):
+    assert _spawn(_grad_worker, kind) == {0: True, 1: True}
+
+
+def test_varlen_plan_host_only():
+    """The plan is built from host lengths alone; the scatter index covers every packed token
+    once and each rank's positions are its sequences'."""
+    lens = [300, 1, 777, 64, 1025]
+    plans = [sh.varlen_plan(lens, lens, 2, r, "cpu") for r in range(2)]
+    nmax = max(plans[0].counts)
+    assert sorted(plans[0].inv.tolist()) == sorted(
+        r * nmax + j for r in range(2) for j in range(plans[0].counts[r]))
+    assert sorted(plans[0].mine_q.tolist() + plans[1].mine_q.tolist()) == list(range(sum(lens)))
+    assert plans[0].cu_q[-1].item() == plans[0].counts[0]
+
+
 @pytest.mark.parametrize("kind", ["heads", "heads_uneven", "heads_alibi", "batch", "batch_pref",
                                   "decode", "varlen"])
 def test_sharded_world2_gloo(kind):

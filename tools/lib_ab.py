@@ -3,6 +3,7 @@
 cdna_hip_programming.md §5.4 rule 24).
 
   python tools/lib_ab.py libA.so libB.so [--mode fwd|bwd] [--rounds 5] [--noncausal]
+  (a build spec may carry options: path@name=val,...; det=1 runs the backward deterministic)
 
 Each path is loaded as its own ctypes library (copy it under a distinct file name first:
 the dynamic loader dedups by soname/path).  Options (--opt name=value) apply to every build.
@@ -42,8 +43,12 @@ def main():
     import shutil
     import tempfile
     libs = []
+    dets = []   # per build: bwd deterministic flag (pseudo-option det=1 in the spec)
     for i, spec in enumerate(a.libs):
         path, _, opts = spec.partition("@")
+        det = any(x == "det=1" for x in opts.split(","))
+        opts = ",".join(x for x in opts.split(",") if x and not x.startswith("det="))
+        dets.append(det)
         if opts:
             tmp = os.path.join(tempfile.mkdtemp(), f"v{i}_" + os.path.basename(path))
             shutil.copy(path, tmp)
@@ -88,6 +93,7 @@ def main():
         dbytes = 2 * int(lens.sum()) * DHK * 128 * kc.element_size()
 
     def run(lib):
+        det = dets[libs.index(lib)]
         if a.mode == "decode":
             lib.fmha_page_kvcache_fwd_ex(P(dq_), P(kc), P(vc), P(do_), P(dlse), P(table), DS // page,
                                          P(lens), 1, DS, DB, DH, DHK, 128, page, 128 ** -0.5, -1, 0,
@@ -101,7 +107,7 @@ def main():
                      sc, None, P(lse), -1, wr, 0.0, False, False, 0)
         if a.mode == "bwd":
             lib.fmha_bwd(P(do), P(q), P(k), P(v), P(o), P(lse), P(dq), P(dk), P(dv), None, None,
-                         a.s, a.s, a.b, a.h, hk, a.d, 0.0, sc, -1, wr, 0.0, False, False, stream,
+                         a.s, a.s, a.b, a.h, hk, a.d, 0.0, sc, -1, wr, 0.0, det, False, stream,
                          None, 0)
 
     # outputs of every build against the first one's (atomic dQ sums differ in the last bits

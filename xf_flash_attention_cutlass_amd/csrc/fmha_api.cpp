@@ -45,6 +45,9 @@ thread_local int g_status = 0;
 thread_local int g_last_splits = 0;     // split count of this thread's last forward launch
 
 void clear_error() { g_err.clear(); g_status = 0; }
+// forward entries: also forget the last forward's kernel / splits, so a call that fails
+// validation or launches nothing reports "" / 0 (fmha_last_kernel's contract)
+void begin_fwd() { clear_error(); g_last_kernel[0] = 0; g_last_splits = 0; }
 bool fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 bool fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -426,7 +429,7 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
               int window_size_left, int window_size_right, const float softcap,
               const bool return_softmax, bool is_fp16, int num_splits) {
     try {
-        clear_error();
+        begin_fwd();
         DevRngScope rng_scope;
         if (!check_common(q_ptr, k_ptr, v_ptr, o_ptr, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
@@ -460,7 +463,7 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
                       float softcap, bool is_fp16, int num_splits, hipStream_t stream,
                       float p_dropout, void* s_dmask) {
     try {
-        clear_error();
+        begin_fwd();
         DevRngScope rng_scope;
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(st != nullptr, "strides must be non-null");
@@ -514,7 +517,7 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
                   float softmax_scale, int window_size_left, int window_size_right, bool out_fp16,
                   hipStream_t stream) {
     try {
-        clear_error();
+        begin_fwd();
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(head_size == 128, "the fp8 forward supports head_size 128 (got %d)", head_size);
         REQUIRE(seqlen_q > 0 && seqlen_k > 0, "seqlen_q/seqlen_k must be positive (%d, %d)", seqlen_q, seqlen_k);
@@ -566,7 +569,7 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
                         int window_size_right, float softcap, bool is_fp16, hipStream_t stream,
                         float p_dropout, void* s_dmask) {
     try {
-        clear_error();
+        begin_fwd();
         DevRngScope rng_scope;
         if (!check_common(q, k, v, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(cu_seqlens_q && (cu_seqlens_k || block_table),
@@ -642,7 +645,7 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
                               int32_t kv_dtype, float k_scale, float v_scale,
                               void* cache_leftpad, bool is_fp16, hipStream_t stream) {
     try {
-        clear_error();
+        begin_fwd();
         if (!check_common(q, kcache, vcache, o, batch_size, num_heads, num_heads_k, head_size)) return;
         REQUIRE(block_table, "block_table must be given for the paged KV path");
         REQUIRE(page_block_size > 0, "page_block_size must be positive");
@@ -739,7 +742,7 @@ void fmha_page_kvcache_fwd(void* q_ptr, void* kcache_ptr, void* vcache_ptr, void
                            void* /*cache_batch_idx_ptr*/, void* /*rotary_cos_ptr*/,
                            void* /*rotary_sin_ptr*/, bool /*is_causal*/,
                            bool /*is_rotary_interleaved*/, bool is_fp16) {
-    if (page_block_size <= 0) { clear_error(); fail(1, "page_block_size must be positive"); return; }
+    if (page_block_size <= 0) { begin_fwd(); fail(1, "page_block_size must be positive"); return; }
     fmha_page_kvcache_fwd_ex(q_ptr, kcache_ptr, vcache_ptr, o_ptr, nullptr, block_table_ptr,
                              max_cache_seq_k / page_block_size, cache_seqlens_k_ptr, seqlen_q,
                              seqlen_k, batch_size, num_heads, num_heads_k, head_size,

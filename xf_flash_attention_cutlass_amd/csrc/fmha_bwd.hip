@@ -28,18 +28,20 @@ static hipError_t launch_bwd_impl(const BwdParams& p, hipStream_t st) {
 
     const bool mask = p.wl >= 0 || p.wr >= 0;
     const bool feat = p.alibi || p.softcap_on || p.cu_seqlens_q || p.cu_seqlens_k || p.drop;
-    void (*kern)(const BwdParams) =
-        p.dq_slices ? fmha_bwd_kernel<HD, T, true, true, true>
-        : mask ? (feat ? fmha_bwd_kernel<HD, T, true, true> : fmha_bwd_kernel<HD, T, true, false>)
-               : (feat ? fmha_bwd_kernel<HD, T, false, true> : fmha_bwd_kernel<HD, T, false, false>);
+    // [mask][feat][deterministic slices] (D > 128: one deterministic instance, MASK = FEAT = true)
+    constexpr bool R = bwd_rmw<HD>();
+    void (*const kerns[2][2][2])(const BwdParams) = {
+        {{fmha_bwd_kernel<HD, T, false, false>, fmha_bwd_kernel<HD, T, !R, !R, true>},
+         {fmha_bwd_kernel<HD, T, false, true>, fmha_bwd_kernel<HD, T, !R, true, true>}},
+        {{fmha_bwd_kernel<HD, T, true, false>, fmha_bwd_kernel<HD, T, true, !R, true>},
+         {fmha_bwd_kernel<HD, T, true, true>, fmha_bwd_kernel<HD, T, true, true, true>}}};
+    void (*kern)(const BwdParams) = kerns[mask][feat][p.dq_slices ? 1 : 0];
     const size_t smem = bwd_smem_bytes<HD>();
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] {
-        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        (void)hipFuncSetAttribute((const void*)fmha_bwd_kernel<HD, T, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        for (int i = 0; i < 8; ++i)
+            (void)hipFuncSetAttribute((const void*)kerns[i >> 2][(i >> 1) & 1][i & 1],
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     });
     const int nkb = (p.seqlen_k + bwd_block_n<HD>() - 1) / bwd_block_n<HD>();
     BwdParams pp = p;

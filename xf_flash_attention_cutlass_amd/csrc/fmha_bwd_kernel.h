@@ -25,6 +25,15 @@
 #pragma once
 
 #include "fmha_common.h"
+#ifndef XFA_BWD_ABL
+#define XFA_BWD_ABL 0   // (timing ablation builds only, tools/quick_variant.py: results INVALID)
+#endif
+#ifndef XFA_RMW_EARLY
+#define XFA_RMW_EARLY 1
+#endif
+#ifndef XFA_BWD_RMW
+#define XFA_BWD_RMW 1   // (A/B builds only: 0 = deterministic slices by float atomics)
+#endif
 
 namespace xfa {
 
@@ -43,6 +52,10 @@ template <int HD> constexpr size_t bwd_smem_bytes() {
     return (bwd_v_in_regs<HD>() ? 1 : 2) * (size_t)bwd_block_n<HD>() * HD * 2 + 2 * (size_t)32 * HD * 2 +
            (size_t)bwd_block_n<HD>() * 64;
 }
+// Deterministic mode adds dQ by read-modify-write of its slice (D <= 128). D > 128 keeps float
+// atomics into the slice, as the only deterministic instance (MASK = FEAT = true): its RMW build
+// faulted on the GPU (r6, 300 x 1100 non-causal) and was not pursued — D = 256 is off the C3 path.
+template <int HD> constexpr bool bwd_rmw() { return XFA_BWD_RMW && HD <= 128; }
 // dQ partial sums -> the fp32 accumulator (deterministic mode: this workgroup's slice, which no
 // other workgroup touches) by float atomics
 __device__ __forceinline__ void dq_add(float v, __amdgpu_buffer_rsrc_t r, int off) {
@@ -120,7 +133,8 @@ __global__ void __launch_bounds__(256) fmha_bwd_pre_kernel(const BwdParams p, in
     if (c == 0) p.dsum[li] = acc;
     float* qa = p.dq_accum + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
                 (int64_t)pos * p.acc_row + d0;
-    const int ns = p.dq_slices ? p.dq_slices : 1;
+    // (deterministic RMW slices are initialised by their own walk: no zeroing here)
+    const int ns = p.dq_slices ? (bwd_rmw<HD>() ? 0 : p.dq_slices) : 1;
     for (int s = 0; s < ns; ++s, qa += p.acc_slice) {
         *reinterpret_cast<f32x4_t*>(qa) = f32x4_t{0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<f32x4_t*>(qa + 4) = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -165,9 +179,14 @@ __global__ void __launch_bounds__(256) fmha_bwd_convert_kernel(const BwdParams p
 // ---------------------------------------------------------------- main ---------------------
 // One key block kb (BN keys) of one (batch, kv head) bh: dK / dV of its keys, dQ partial sums
 // added into dq_base (the accumulator, or this workgroup's deterministic slice).
-template <int HD, typename T, bool MASK, bool FEAT>
+// RMW (deterministic mode): dq_base is a slice this workgroup alone writes, so the dQ partial
+// sums are added by plain read-modify-write instead of float atomics: the tile's slice values
+// are loaded at the top of the iteration (with the next tile's Q / dO) and the sums stored
+// back as 16-byte rows at its end (dQ^T = K^T dS^T on the MFMA puts 4 consecutive head-dim
+// columns of one query row on a lane)
+template <int HD, typename T, bool MASK, bool FEAT, bool RMW = false>
 __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, const int bh, const int kb,
-                                              float* const dq_base) {
+                                              float* const dq_base, const bool first = false) {
     using V8 = typename DT<T>::v8;
     constexpr int NW = bwd_waves<HD>();
     constexpr int BN = bwd_block_n<HD>();
@@ -214,7 +233,6 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
         if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
         if (p.cu_seqlens_k) { k_off = p.cu_seqlens_k[bidx]; sk = p.cu_seqlens_k[bidx + 1] - k_off; }
     }
-    if (n0 >= sk) return;
     const int diag = sk - sq;
 
     // query positions that can see any key of [n0, n0 + BN)
@@ -222,7 +240,27 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
     if (MASK && p.wr >= 0) p_lo = max(0, n0 - diag - p.wr);
     if (MASK && p.wl >= 0) p_hi = min(sq, n0 + BN - 1 - diag + p.wl + 1);
     const int t_lo = p_lo / BQ;
-    const int ntiles = p_hi > p_lo ? (p_hi + BQ - 1) / BQ - t_lo : 0;
+    const int ntiles = n0 < sk && p_hi > p_lo ? (p_hi + BQ - 1) / BQ - t_lo : 0;
+    if constexpr (RMW) {
+        // the first block of a slice's walk initialises the slice: its tiles [t_lo, t_lo +
+        // ntiles) get plain stores of their sums (no read) below, every other row of the G heads
+        // zeros here, so later blocks can read-modify-write any row (no zeroing pass)
+        if (first) {
+            constexpr int C4 = HD / 4;   // 16-byte chunks per accumulator row
+            const int r0 = t_lo * BQ, r1 = min(sq, (t_lo + ntiles) * BQ);
+            const int nz = ntiles ? sq - (r1 - r0) : sq;
+            for (int i = threadIdx.x; i < p.group * nz * C4; i += NW * 64) {
+                const int g = i / (nz * C4), rem = i - g * nz * C4;
+                int row = rem / C4;
+                const int c = rem - row * C4;
+                if (ntiles && row >= r0) row += r1 - r0;
+                float* dst = dq_base + (int64_t)bidx * p.acc_batch + (int64_t)(hk_i * p.group + g) * p.acc_head +
+                             (int64_t)(q_off + row) * p.acc_row + 4 * c;
+                *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+    if (n0 >= sk) return;
     const int G = p.group;
     const int n_iter = ntiles * G;
 
@@ -408,6 +446,18 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
         const int tt = p.desc ? (g + 1) * ntiles - 1 - it : it - g * ntiles;
         const int head = hk_i * G + g;
         const int q0 = (t_lo + tt) * BQ;
+        // RMW: this tile's rows of the dQ slice (rows past the end / padded columns read as
+        // zeros and their stores are dropped by the descriptor bounds) and this lane's offsets
+        auto dq_rsrc = [&]() {
+            const float* t = dq_base + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
+                             (int64_t)(q_off + q0) * p.acc_row;
+            return make_rsrc(t, (uint32_t)(max(0, sq - q0) * p.acc_row * 4));
+        };
+        auto dq_off = [&](const int i) {
+            const int d = 16 * ((wave >> 1) * NDQ + i) + 4 * g16;
+            return d < p.d ? (16 * mt + (lane & 15)) * (int)p.acc_row * 4 + d * 4 : kOOB;
+        };
+        f32x4 dq_old[RMW ? NDQ : 1];
         // this tile's LSE / D -> a private slot in this wave's own dS^T rows (nobody reads
         // them before this wave's dS^T store; the other waves' dQ reads ended at the last
         // barrier), read back below as broadcast float4s
@@ -418,6 +468,12 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
         // them pending across the back-edge and waited vmcnt at the loop head, retiring the
         // previous tile's dQ atomics there)
         if (!VR) load_q(min(it + 1, n_iter - 1));
+        if constexpr (RMW && XFA_RMW_EARLY) {
+            const __amdgpu_buffer_rsrc_t rs = dq_rsrc();
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i)
+                dq_old[i] = first || XFA_BWD_ABL == 1 ? f32x4{} : __builtin_bit_cast(f32x4, buf_load16(rs, dq_off(i)));
+        }
 
         // ---- S = Q K^T and dP = dO V^T (key on the lane, query rows in registers)
         f32x16 s_acc[KS], dp_acc[KS];
@@ -547,6 +603,14 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
                 if constexpr (HD > 128) __builtin_amdgcn_sched_barrier(0);
             }
         }
+        // RMW: the slice's current values of this tile (issued after the S / dP register peak;
+        // the dS^T store, the barrier and the dQ product cover their latency)
+        if constexpr (RMW && !XFA_RMW_EARLY) {
+            const __amdgpu_buffer_rsrc_t rs = dq_rsrc();
+#pragma unroll
+            for (int i = 0; i < NDQ; ++i)
+                dq_old[i] = first ? f32x4{} : __builtin_bit_cast(f32x4, buf_load16(rs, dq_off(i)));
+        }
         // ---- dS^T -> LDS (bf16/f16): row = key (this lane), 4 consecutive q per store
         {
             typedef __attribute__((ext_vector_type(4))) T T4;
@@ -584,10 +648,25 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
                     const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         (lds_s16x4*)(size_t)(dqb(i, 1) + ks * 32 * HD * 2));
                     const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-                    dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
+                    // (RMW: dQ^T[d][q] = K^T dS^T, the operands swapped: a lane holds 4
+                    // consecutive d of query row lane & 15)
+                    if constexpr (RMW) dq[i] = DT16<T>::mfma16(__builtin_bit_cast(V8, bv), a, dq[i]);
+                    else dq[i] = DT16<T>::mfma16(a, __builtin_bit_cast(V8, bv), dq[i]);
                 }
                 if constexpr (HD > 128) __builtin_amdgcn_sched_barrier(0);
             }
+            if constexpr (RMW) {
+                const __amdgpu_buffer_rsrc_t rs = dq_rsrc();
+#pragma unroll
+                for (int i = 0; i < NDQ; ++i) {
+                    const f32x4 v = dq_old[i] + dq[i];
+#if defined(XFA_BWD_ABL) && XFA_BWD_ABL == 1
+                    asm volatile("" :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));   // (timing ablation)
+#else
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, dq_off(i), 0, 0);
+#endif
+                }
+            } else {
             // buffer atomics over this (batch, head)'s rows [q0, sq): rows past the end and the
             // padded head-dim columns fall outside the descriptor and are dropped (no branches)
             const float* qa = dq_base + (int64_t)bidx * p.acc_batch + (int64_t)head * p.acc_head +
@@ -602,6 +681,7 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     dq_add(dq[i][r], qrs, base + r * arow);
+            }
             }
         }
         __syncthreads();
@@ -634,24 +714,28 @@ __device__ __forceinline__ void bwd_key_block(const BwdParams& p, char* smem, co
     }
 }
 
-// DET (deterministic dQ) is instantiated only with MASK = FEAT = true, whose runtime tests cover
-// every window / feature combination.
 template <int HD, typename T, bool MASK, bool FEAT, bool DET = false>
 __global__ void __launch_bounds__(bwd_waves<HD>() * 64, bwd_waves<HD>() / 4) fmha_bwd_kernel(const BwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BN = bwd_block_n<HD>();
     const int nkb = (p.seqlen_k + BN - 1) / BN;
     if constexpr (DET) {
-        // workgroup (bh, s) owns dQ slice s and walks key blocks s, s + S, s + 2S, ... (S =
-        // gridDim.y slices) in order; each block's atomics are retired (vmcnt(0)) before the
-        // next block issues its own, so every dQ element receives its adds in key-block order
-        float* const slice = p.dq_accum + (int64_t)blockIdx.y * p.acc_slice;
-        for (int kb = (int)blockIdx.y; kb < nkb; kb += (int)gridDim.y) {
-            if (kb != (int)blockIdx.y) {
+        // workgroup (bh, s) alone owns dQ slice s and walks the key blocks of round r = 0, 1, ...
+        // in order: block r*S + s in even rounds, r*S + S-1-s in odd ones (S = gridDim.y
+        // slices; the snake evens out the causal work per slice). Its dQ adds are plain
+        // read-modify-writes of the slice; each block's stores are retired (vmcnt(0)) before the
+        // next block reads the same rows, so every dQ element receives its adds in key-block
+        // order from one lane
+        const int S = (int)gridDim.y, s = (int)blockIdx.y;
+        float* const slice = p.dq_accum + (int64_t)s * p.acc_slice;
+        for (int r = 0;; ++r) {
+            const int kb = r * S + ((r & 1) ? S - 1 - s : s);
+            if (kb >= nkb) break;
+            if (r) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
             }
-            bwd_key_block<HD, T, MASK, FEAT>(p, smem, (int)blockIdx.x, kb, slice);
+            bwd_key_block<HD, T, MASK, FEAT, bwd_rmw<HD>()>(p, smem, (int)blockIdx.x, kb, slice, r == 0);
         }
     } else {
         // order 1: workgroup w runs on XCD w % 8 (dispatch round-robin); XCD x takes the kv

@@ -15,7 +15,8 @@
 // returns it) instead of being silently ignored.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
-#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
 #include <ATen/hip/HIPGeneratorImpl.h>
 
 #include <limits>
@@ -33,7 +34,7 @@ void raise_if_failed(const char* op) {
     if (fmha_last_status() != 0) TORCH_CHECK(false, op, ": ", fmha_last_error());
 }
 
-hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 int round8(int x) { return (x + 7) / 8 * 8; }
 
@@ -85,7 +86,9 @@ at::Tensor alibi_for_c(c10::optional<at::Tensor>& a, int b, int h, int64_t* bstr
     return s;
 }
 
-// Dropout: the key from torch's HIP generator as philox_cuda_state (export.cpp:616-627,
+// Dropout: the key from torch's HIP generator (ATen/hip/HIPGeneratorImpl.h, whose generator
+// class and Philox state keep their upstream names in this ROCm build: CUDAGeneratorImpl,
+// PhiloxCudaState — no other spelling exists) as philox_cuda_state (export.cpp:616-627,
 // flash_api_hip.cpp:509): outside stream capture the host seed / offset; under capture the
 // generator's device seed / offset pointers, read by the kernels when the graph runs (so every
 // replay draws a fresh mask).  rng_state is an int64 [2] on q's device, as upstream returns it;
@@ -194,7 +197,7 @@ mha_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v, c10::optional<a
         out = torch::empty_like(q_padded, at::MemoryFormat::Contiguous);
     }
     const int head_size = round8(head_size_og);
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto opts = q.options();
     auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, seqlen_q, seqlen_k);
@@ -308,7 +311,7 @@ mha_varlen_fwd(at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
         out = torch::empty_like(q_padded);
     }
     const int head_size = round8(head_size_og);
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto opts = q.options();
     auto softmax_lse = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
     at::Tensor p = sdmask_buffer(return_softmax, opts, batch_size, num_heads, max_seqlen_q, max_seqlen_k);
@@ -422,7 +425,7 @@ mha_fwd_kvcache(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& vcach
         out = torch::empty_like(q_padded);
     }
     const int head_size = round8(head_size_og);
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto opts = q.options();
     auto softmax_lse = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     at::Tensor seqlens;
@@ -570,7 +573,7 @@ mha_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const 
     CHECK_SHAPE(softmax_lse, batch_size, num_heads, seqlen_q);
     at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
     at::Tensor dout_padded = dense(pad_last(dout, head_size_og));
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto opts = q.options();
     auto softmax_d = torch::empty({batch_size, num_heads, seqlen_q}, opts.dtype(at::kFloat));
     int64_t alibi_bs = 0;
@@ -636,7 +639,7 @@ mha_varlen_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     CHECK_SHAPE(dout, total_q, num_heads, head_size_og);
     at::Tensor dq = grad_out(dq_, q), dk = grad_out(dk_, k), dv = grad_out(dv_, v);
     at::Tensor dout_padded = dense(pad_last(dout, head_size_og));
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto opts = q.options();
     auto softmax_d = torch::empty({num_heads, total_q}, opts.dtype(at::kFloat));
     int64_t alibi_bs = 0;
@@ -692,7 +695,7 @@ mha_fwd_kvcache_fp8(at::Tensor& q, const at::Tensor& kcache, const at::Tensor& v
     if (is_causal) window_size_right = 0;
     if (window_size_left >= seqlen_k) window_size_left = -1;
     if (window_size_right >= seqlen_k) window_size_right = -1;
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     auto qc = dense(q);
     auto out = torch::empty_like(qc);
     auto lse = torch::empty({batch_size, num_heads, seqlen_q}, q.options().dtype(at::kFloat));
@@ -729,7 +732,7 @@ mha_fwd_fp8(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     if (is_causal) window_size_right = 0;
     if (window_size_left >= seqlen_k) window_size_left = -1;
     if (window_size_right >= seqlen_k) window_size_right = -1;
-    at::hip::HIPGuardMasqueradingAsCUDA device_guard{(char)q.get_device()};
+    const c10::DeviceGuard device_guard(q.device());
     const auto odt = out_fp16 ? torch::kFloat16 : torch::kBFloat16;
     at::Tensor out;
     if (out_.has_value()) {

@@ -89,31 +89,22 @@ def _slice_alibi(alibi, heads: Shard | None = None, batch: Shard | None = None):
     return alibi.contiguous()
 
 
-def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
-    """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank.
-
-    Even shards (the usual case: heads or batch divisible by the world size): along dim 0 one
-    all_gather_into_tensor whose rank-major buffer IS the result (no copy); along another dim
-    (head shards) the ranks' pieces are gathered straight into their strided views of the
-    assembled output (RCCL lands them in its staging buffer, which torch then scatters into the
-    views: no intermediate [world, ...] tensor and no reshape copy).  Uneven shards pad to the
-    largest piece along `dim` and drop the padding afterwards."""
-    dist, rank, world = _world()
-    if world == 1:
-        return local
+def _gather_dim_impl(local: torch.Tensor, sizes: Sequence[int], dim: int, dist, world: int):
+    """The collective itself (world > 1).  Even shards: along dim 0 one all_gather_into_tensor
+    whose rank-major buffer IS the result; along another dim (head shards) the rank-major
+    buffer is moved to `dim` with one copy.  Uneven shards pad to the largest piece along `dim`
+    and drop the padding afterwards."""
     local = local.contiguous()
     nmax = max(sizes)
-    if min(sizes) == nmax:
-        shape = list(local.shape)
-        if dim == 0:
-            gathered = local.new_empty([world * shape[0]] + shape[1:])  # rank-major along dim 0
-            dist.all_gather_into_tensor(gathered, local)
-            return gathered
-        shape[dim] = world * nmax
-        out = local.new_empty(shape)
-        dist.all_gather(list(out.split(nmax, dim=dim)), local)
-        return out
     shape = list(local.shape)
+    if min(sizes) == nmax:
+        gathered = local.new_empty([world * shape[0]] + shape[1:])   # rank-major along dim 0
+        dist.all_gather_into_tensor(gathered, local)
+        if dim == 0:
+            return gathered
+        # [world, *shape] -> pieces side by side along dim
+        g = gathered.view([world] + shape).movedim(0, dim)
+        return g.reshape(shape[:dim] + [world * nmax] + shape[dim + 1:])
     shape[dim] = nmax
     buf = local.new_zeros(shape)
     buf.narrow(dim, 0, local.shape[dim]).copy_(local)
@@ -121,6 +112,34 @@ def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
     dist.all_gather_into_tensor(gathered, buf)
     gathered = gathered.view([world] + shape)
     return torch.cat([gathered[r].narrow(dim, 0, sizes[r]) for r in range(world)], dim=dim)
+
+
+class _AllGatherDim(torch.autograd.Function):
+    """All-gather along `dim` whose backward hands each rank the gradient of its own piece.
+
+    Every rank holds the whole gathered output and (data-parallel replicas of one step) computes
+    the same loss from it, so d loss / d (my piece) is the slice of d loss / d out at my offset:
+    the backward is a narrow, with no communication."""
+
+    @staticmethod
+    def forward(ctx, local, sizes, dim, rank):
+        dist, _, world = _world()
+        ctx.dim, ctx.start, ctx.size = dim, sum(sizes[:rank]), sizes[rank]
+        return _gather_dim_impl(local, sizes, dim, dist, world)
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad.narrow(ctx.dim, ctx.start, ctx.size), None, None, None
+
+
+def all_gather_dim(local: torch.Tensor, sizes: Sequence[int], dim: int):
+    """Concatenate per-rank pieces along `dim` (rank r holds sizes[r] entries) on every rank.
+    Differentiable (`_AllGatherDim`): the backward narrows the output gradient to this rank's
+    piece.  World size 1 runs no collective: the local piece is the result."""
+    dist, rank, world = _world()
+    if world == 1:
+        return local
+    return _AllGatherDim.apply(local, list(sizes), dim, rank)
 
 
 def sharded_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
@@ -172,50 +191,111 @@ def attention_shards(batch: int, num_heads: int, num_heads_k: int, world: int,
     return "batch", batch_shards(batch, world)
 
 
-def sharded_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, local_fn: Callable | None = None,
-                   gather: bool = True, **kw):
+@dataclass(frozen=True)
+class VarlenPlan:
+    """Sequence shards of one packed varlen batch, built once from HOST-side lengths (no device
+    sync when it is reused): every rank can compute every rank's part, so the per-rank token
+    counts need no exchange.
+
+    mine_q / mine_k : packed positions of this rank's query / key tokens (device, int64)
+    cu_q / cu_k     : this rank's local cumulative lengths (device, int32)
+    max_q / max_k   : this rank's longest sequences (0 if it has none)
+    counts          : query tokens per rank;  inv: for each packed query position, its row in the
+                      rank-major gathered [world * max(counts)] buffer (device, int64)"""
+    parts: tuple
+    mine_q: torch.Tensor
+    mine_k: torch.Tensor
+    cu_q: torch.Tensor
+    cu_k: torch.Tensor
+    max_q: int
+    max_k: int
+    counts: tuple
+    inv: torch.Tensor
+
+
+def varlen_plan(seqlens_q: Sequence[int], seqlens_k: Sequence[int], world: int, rank: int,
+                device) -> VarlenPlan:
+    """Plan for `sharded_varlen` from host lengths (lists of ints), balanced on s_q * s_k."""
+    lq = [int(x) for x in seqlens_q]
+    lk = [int(x) for x in seqlens_k]
+    parts = balanced_sequences(lq, lk, world)
+    cq = [0]
+    ck = [0]
+    for a, b in zip(lq, lk):
+        cq.append(cq[-1] + a)
+        ck.append(ck[-1] + b)
+
+    def positions(seqs, cu):
+        return [t for i in seqs for t in range(cu[i], cu[i + 1])]
+    counts = [sum(lq[i] for i in p) for p in parts]
+    nmax = max(counts) if counts else 0
+    inv = [0] * cq[-1]
+    for r, p in enumerate(parts):
+        for j, t in enumerate(positions(p, cq)):
+            inv[t] = r * nmax + j
+    mine = parts[rank]
+
+    def cum(lens):
+        out = [0]
+        for x in lens:
+            out.append(out[-1] + x)
+        return out
+    L = lambda xs: torch.tensor(xs, dtype=torch.long, device=device)  # noqa: E731
+    return VarlenPlan(
+        parts=tuple(tuple(p) for p in parts),
+        mine_q=L(positions(mine, cq)), mine_k=L(positions(mine, ck)),
+        cu_q=torch.tensor(cum([lq[i] for i in mine]), dtype=torch.int32, device=device),
+        cu_k=torch.tensor(cum([lk[i] for i in mine]), dtype=torch.int32, device=device),
+        max_q=max([lq[i] for i in mine], default=0), max_k=max([lk[i] for i in mine], default=0),
+        counts=tuple(counts), inv=L(inv))
+
+
+class _GatherPacked(torch.autograd.Function):
+    """All-gather of per-rank packed outputs back into the global packed order (rank-major
+    buffer padded to the largest count, then one index_select).  Backward: this rank's rows of
+    the output gradient, no communication (as `_AllGatherDim`)."""
+
+    @staticmethod
+    def forward(ctx, local, plan):
+        dist, rank, world = _world()
+        ctx.mine = plan.mine_q
+        nmax = max(plan.counts)
+        buf = local.new_zeros((nmax,) + tuple(local.shape[1:]))
+        buf[: local.shape[0]] = local
+        gathered = local.new_empty((world * nmax,) + tuple(local.shape[1:]))
+        dist.all_gather_into_tensor(gathered, buf)
+        return gathered.index_select(0, plan.inv)
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad.index_select(0, ctx.mine), None
+
+
+def sharded_varlen(q, k, v, cu_seqlens_q=None, cu_seqlens_k=None, local_fn: Callable | None = None,
+                   gather: bool = True, plan: VarlenPlan | None = None, **kw):
     """Sequence-sharded varlen attention (C4): ranks take whole sequences, balanced on
-    s_q*s_k; outputs are all-gathered back into the packed [total_q, H, d] order."""
+    s_q*s_k; outputs are all-gathered back into the packed [total_q, H, d] order.  Pass a
+    `plan` (`varlen_plan`, from host-side lengths) to run without any device sync; without
+    one it is built from `cu_seqlens_*` (one host copy of each).  Differentiable: gradients
+    flow to this rank's tokens of q / k / v.  Returns (out, packed positions of my tokens)."""
     dist, rank, world = _world()
     if local_fn is None:
         from . import flash_attn_varlen_func as local_fn
-    cq = [int(x) for x in cu_seqlens_q.tolist()]
-    ck = [int(x) for x in cu_seqlens_k.tolist()]
-    lq = [b - a for a, b in zip(cq[:-1], cq[1:])]
-    lk = [b - a for a, b in zip(ck[:-1], ck[1:])]
-    parts = balanced_sequences(lq, lk, world)
-    mine = parts[rank]
-    dev = q.device
-    if mine:
-        qi = torch.cat([torch.arange(cq[i], cq[i + 1]) for i in mine]).to(dev)
-        ki = torch.cat([torch.arange(ck[i], ck[i + 1]) for i in mine]).to(dev)
-        cql = torch.tensor([0] + list(torch.tensor([lq[i] for i in mine]).cumsum(0).tolist()),
-                           dtype=torch.int32, device=dev)
-        ckl = torch.tensor([0] + list(torch.tensor([lk[i] for i in mine]).cumsum(0).tolist()),
-                           dtype=torch.int32, device=dev)
-        out_local = local_fn(q[qi], k[ki], v[ki], cql, ckl, max(lq[i] for i in mine),
-                             max(lk[i] for i in mine), **kw)
+    if plan is None:
+        cq = [int(x) for x in cu_seqlens_q.tolist()]
+        ck = [int(x) for x in cu_seqlens_k.tolist()]
+        plan = varlen_plan([b - a for a, b in zip(cq[:-1], cq[1:])],
+                           [b - a for a, b in zip(ck[:-1], ck[1:])], world, rank, q.device)
+    if plan.mine_q.numel():
+        out_local = local_fn(q.index_select(0, plan.mine_q), k.index_select(0, plan.mine_k),
+                             v.index_select(0, plan.mine_k), plan.cu_q, plan.cu_k, plan.max_q,
+                             plan.max_k, **kw)
     else:
-        qi = torch.empty(0, dtype=torch.long, device=dev)
-        out_local = q.new_empty((0,) + tuple(q.shape[1:]))
+        # no sequences on this rank: a zero-row output still tied to q for autograd
+        out_local = q.narrow(0, 0, 0) * 0
     if not gather or world == 1:
-        return out_local, qi
-    # pad to the largest local token count, gather, then scatter back into packed order
-    n_local = torch.tensor([out_local.shape[0]], device=dev)
-    counts = [torch.zeros_like(n_local) for _ in range(world)]
-    dist.all_gather(counts, n_local)
-    nmax = int(max(c.item() for c in counts))
-    buf = q.new_zeros((nmax,) + tuple(q.shape[1:]))
-    buf[: out_local.shape[0]] = out_local
-    gathered = q.new_empty((world * nmax,) + tuple(q.shape[1:]))
-    dist.all_gather_into_tensor(gathered, buf)
-    gathered = gathered.view((world, nmax) + tuple(q.shape[1:]))
-    out = q.new_empty(q.shape)
-    for r in range(world):
-        idx = torch.cat([torch.arange(cq[i], cq[i + 1]) for i in parts[r]]).to(dev) if parts[r] \
-            else torch.empty(0, dtype=torch.long, device=dev)
-        out[idx] = gathered[r, : idx.numel()]
-    return out, qi
+        return out_local, plan.mine_q
+    return _GatherPacked.apply(out_local, plan), plan.mine_q
 
 
 def batch_shards(batch: int, world: int) -> List[Shard]:
