@@ -75,6 +75,10 @@ def parse(argv=None):
     ap.add_argument("--seqlen", type=int, default=0, help="default: 4096 (fwd), 32768 (decode)")
     ap.add_argument("--headdim", type=int, default=128)
     ap.add_argument("--no-causal", action="store_true")
+    ap.add_argument("--alibi", action="store_true",
+                    help="fwd/fwdbwd: ALiBi slopes 2^(-8 (h+1) / H) (the standard geometric set)")
+    ap.add_argument("--window-left", type=int, default=-1,
+                    help="fwd/fwdbwd: left window (causal + wl = a sliding window of wl + 1 keys)")
     ap.add_argument("--ragged", action="store_true", help="decode: cache lengths U[1, S]")
     ap.add_argument("--rotate", type=int, default=0,
                     help="input sets cycled step by step (default: 2 for fwd/fwdbwd, so every "
@@ -254,21 +258,28 @@ def workload_dense(a, mode, dev, rank, world):
         sets.append((q, k, v, out, dout))
     nxt = _rotating(sets)
     res = {}
+    wl = a.window_left
+    alibi = (torch.tensor([2.0 ** (-8.0 * (i + 1) / H) for i in range(H)], device=dev)[:Hr]
+             if a.alibi else None)
 
     def fwd():
         q, k, v, out, _ = nxt()
-        res["r"] = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
+        res["r"] = pa.fwd(q, k, v, out, alibi, 0.0, scale, causal, wl, -1, 0.0, False, None)
 
     def fwdbwd():
         q, k, v, out, dout = nxt()
-        r = pa.fwd(q, k, v, out, None, 0.0, scale, causal, -1, -1, 0.0, False, None)
-        pa.bwd(dout, q, k, v, out, r[5], None, None, None, None, 0.0, scale, causal, -1, -1,
+        r = pa.fwd(q, k, v, out, alibi, 0.0, scale, causal, wl, -1, 0.0, False, None)
+        pa.bwd(dout, q, k, v, out, r[5], None, None, None, alibi, 0.0, scale, causal, wl, -1,
                0.0, False, None, None)
         res["r"] = r
 
     ff = fwd_flops(B, Hr, S, S, D, causal)
+    if wl >= 0:    # (sq = sk) row pos sees keys max(0, pos - wl) .. pos (causal) or .. pos + wl
+        vis = sum(min(p, wl) + 1 + (0 if causal else min(S - 1 - p, wl)) for p in range(S))
+        ff = 4.0 * B * Hr * D * vis
     mult = 3.5 if mode == "fwdbwd" else 1.0
-    cs = "causal" if causal else "non-causal"
+    cs = ("causal" if causal else "non-causal") + (" ALiBi" if a.alibi else "") + \
+        (f" window ({wl}, {0 if causal else wl})" if wl >= 0 else "")
     glob_b = B * world if a.scaling == "weak" else B
     return dict(step=fwd if mode == "fwd" else fwdbwd, units=ff * mult, bound="mfma",
                 out=lambda: sets[0][3], gather_dim=0 if a.scaling == "weak" else 2,
@@ -590,7 +601,7 @@ def sub_result(a, mode, dev, stream, **over):
     out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
            "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
            "unit": "GB/s" if hbm else "TFLOP/s",
-           "roofline": roofline(w, ev, mode + ("_ragged" if a.ragged else "")),
+           "roofline": roofline(w, ev, getattr(a, "roof_key", None) or mode + ("_ragged" if a.ragged else "")),
            "kernel": last_kernel(),
            "gpu_clock": clock_stats(t_pw + 0.2, t_end)}
     if not a.no_cpu_baseline:
@@ -779,6 +790,15 @@ def run(a, world, rank, local):
         extras["decode"] = sub_result(a, "decode", dev, stream)
         extras["decode_ragged"] = sub_result(a, "decode", dev, stream, ragged=True)
         extras["fwd_fp8"] = sub_result(a, "fwd_fp8", dev, stream)
+        # north_star's target shape names no mask: the same C2 shape non-causal; and the C2 shape
+        # with the two masks the reference's kernel also takes, causal ALiBi and a causal
+        # 1024-key sliding window (no CPU baselines for these three)
+        extras["fwd_noncausal"] = sub_result(a, "fwd", dev, stream, no_causal=True,
+                                             no_cpu_baseline=True, roof_key="fwd_noncausal")
+        extras["fwd_alibi"] = sub_result(a, "fwd", dev, stream, alibi=True, no_cpu_baseline=True,
+                                         roof_key="fwd_alibi")
+        extras["fwd_window"] = sub_result(a, "fwd", dev, stream, window_left=1023,
+                                          no_cpu_baseline=True, roof_key="fwd_window")
     if dist:
         dist.barrier()
 

@@ -100,6 +100,17 @@ def alibi_bias(slopes: torch.Tensor, seqlen_q: int, seqlen_k: int,
     return -s * dist.to(slopes.dtype)
 
 
+def alibi_bias_kernel(slopes: torch.Tensor, seqlen_q: int, seqlen_k: int, causal=False,
+                      key_padding_mask=None) -> torch.Tensor:
+    """ALiBi bias in the reference KERNEL's form (mask_hip.h:162-167), for the LSE the kernel
+    returns: causal `+slope * col` (test.py's oracle uses slope * (col - sk + 1), a per-row
+    constant apart: equal O, different LSE); otherwise `-slope * |row + sk - sq - col|`."""
+    if not causal:
+        return alibi_bias(slopes, seqlen_q, seqlen_k, None, key_padding_mask, causal=False)
+    b, h = slopes.shape
+    return torch.arange(seqlen_k, device=slopes.device, dtype=torch.float32) * slopes.view(b, h, 1, 1)
+
+
 def expand_kv(x: torch.Tensor, nheads: int) -> torch.Tensor:
     """[b, s, hk, d] -> [b, s, nheads, d]; query head i reads kv head i // (nheads/hk)."""
     g = nheads // x.shape[2]
@@ -163,9 +174,10 @@ def attention_lse_ref(q, k, key_padding_mask=None, attn_bias=None, causal=False,
     This is the quantity the fwd kernel writes to `softmax_lse`
     (`LSE = m*scale + log(sum)`, softmax_hip.h:129-189).  Fully masked rows give
     +inf, the kernel's empty-row convention (flash_fwd_kernel_hip.h:626-670).
-    ALiBi: `attn_bias` must be the non-causal |i+sk-sq-j| form for the kernel's
-    LSE (the causal form of test.py:247-273 differs from it by a per-row constant
-    that cancels in O but not in LSE) — see DESIGN.md §numerics.
+    ALiBi: pass `alibi_bias_kernel(...)`, the reference kernel's form (causal
+    +slope*col, mask_hip.h:163-164), which the build's LSE follows (the causal form
+    of test.py:247-273 differs from it by a per-row constant that cancels in O but
+    not in LSE) — see DESIGN.md §4.
     """
     if causal:
         window_size = (window_size[0], 0)

@@ -18,6 +18,7 @@ import torch
 
 import bench
 from oracle import attention_ref as orc
+from tests import test_fwd4_redo_gpu as r4
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -57,8 +58,8 @@ def test_c2_full_shape(xfa, parity_report):
     torch.cuda.synchronize()
     assert _lib().fmha_last_num_splits() == 1
     kern = _lib().fmha_last_kernel().decode()
-    want = {0: "fmha_fwd_kernel", 1: "fmha_fwd4_kernel", 2: "fmha_fwdpp_kernel"}
-    assert kern.startswith(want[_lib().fmha_get_option(b"fwd_w4")]), kern
+    want = r4.expected_kernel(_lib().fmha_get_option(b"fwd_w4"), 0)     # causal
+    assert kern.startswith(want + " "), kern
     for b, h in SAMPLE_BH:
         qs, ks, vs = (x[b:b + 1, :, h:h + 1].cpu() for x in (q, k, v))
         ref, _ = orc.attention_ref(qs, ks, vs, causal=True)

@@ -65,18 +65,27 @@ def _fwd(q, k, v, causal, window=(-1, -1)):
     capi.check()
     torch.cuda.synchronize()
     assert _lib().fmha_last_num_splits() == 1
-    _assert_fwd4()
+    _assert_fwd4(wr)
     return o.cpu(), lse.cpu()
 
 
-def _assert_fwd4():
+def expected_kernel(w4, wr):
+    """the kernel fwd_w4 = w4 selects for a call with right window wr (4, auto: the 16x16x32
+    ping-pong where no row has a right window, else the 32x32x16 one)"""
+    if w4 == 4:
+        w4 = 3 if wr < 0 else 2
+    return {0: "fmha_fwd_kernel", 1: "fmha_fwd4_kernel", 2: "fmha_fwdpp_kernel",
+            3: "fmha_fwdpp16_kernel"}[w4]
+
+
+def _assert_fwd4(wr=0):
     """the redo asm runs only in the generated D = 128 kernels: prove the one asked for ran
-    (fwd_w4 = 1 the 4-wave kernel, 2 the ping-pong kernel; 0 under XFA_TEST_OPTIONS=fwd_w4=0,
-    the compiler-scheduled 8-wave kernel)"""
+    (fwd_w4 = 1 the 4-wave kernel, 2 / 3 the ping-pong kernels, 4 auto; 0 under
+    XFA_TEST_OPTIONS=fwd_w4=0, the compiler-scheduled 8-wave kernel)"""
     L = _lib()
     kern = L.fmha_last_kernel().decode()
-    want = {0: "fmha_fwd_kernel", 1: "fmha_fwd4_kernel", 2: "fmha_fwdpp_kernel"}
-    assert kern.startswith(want[L.fmha_get_option(b"fwd_w4")]), kern
+    want = expected_kernel(L.fmha_get_option(b"fwd_w4"), wr)
+    assert kern.startswith(want + " "), kern
 
 
 def _check(o, lse, q, k, v, causal, what, rtol_lse=0.0, o_atol=None):
@@ -190,7 +199,7 @@ def test_fwd4_slack0_varlen(xfa, dtype, causal):
         out, lse, _ = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV),
                                                  cu.to(DEV), max(lens), max(lens), causal=causal,
                                                  return_attn_probs=True)
-        _assert_fwd4()
+        _assert_fwd4(0 if causal else -1)
     torch.cuda.synchronize()
     out, lse = out.cpu(), lse.cpu()
     for i in range(len(lens)):

@@ -45,8 +45,8 @@ def test_fwd_golden(xfa, name):
     torch.cuda.synchronize()
     _assert_parity(out, t["out_ref"], t["out_pt"], what=name)
     bias = None
-    if m["alibi"]:
-        bias = orc.alibi_bias(t["alibi_slopes"], m["sq"], m["sk"], causal=False)
+    if m["alibi"]:   # the reference kernel's ALiBi form (causal: +slope*col, mask_hip.h:163-164)
+        bias = orc.alibi_bias_kernel(t["alibi_slopes"], m["sq"], m["sk"], causal=m["causal"])
     lse_ref = orc.attention_lse_ref(t["q"], t["k"], attn_bias=bias, causal=m["causal"],
                                     window_size=tuple(m["window"]), softcap=m["softcap"])
     fin = torch.isfinite(lse_ref)

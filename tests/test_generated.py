@@ -1,6 +1,7 @@
 """CPU: the committed hand-scheduled asm bodies are exactly what their generators emit with the
 default settings (tools/gen_fwd4.py -> fmha_fwd4_body.h, tools/gen_fwd8.py -> fmha_fwd8_body.h,
-tools/gen_fwdpp.py -> fmha_fwdpp_body.h, tools/gen_fwd8pp.py -> fmha_fwd8pp_body.h),
+tools/gen_fwdpp.py -> fmha_fwdpp_body.h, tools/gen_fwdpp16.py -> fmha_fwdpp16_body.h,
+tools/gen_fwd8pp.py -> fmha_fwd8pp_body.h),
 so a review of the generator is a review of the shipped kernel."""
 import os
 import subprocess
@@ -15,11 +16,12 @@ CSRC = os.path.join(ROOT, "xf_flash_attention_cutlass_amd", "csrc")
 @pytest.mark.parametrize("gen,body", [("gen_fwd4.py", "fmha_fwd4_body.h"),
                                       ("gen_fwd8.py", "fmha_fwd8_body.h"),
                                       ("gen_fwdpp.py", "fmha_fwdpp_body.h"),
+                                      ("gen_fwdpp16.py", "fmha_fwdpp16_body.h"),
                                       ("gen_fwd8pp.py", "fmha_fwd8pp_body.h")])
 def test_generated_body_matches_generator(tmp_path, gen, body):
     out = tmp_path / body
     args = [sys.executable, os.path.join(ROOT, "tools", gen)]
-    if gen in ("gen_fwd4.py", "gen_fwdpp.py", "gen_fwd8pp.py"):
+    if gen in ("gen_fwd4.py", "gen_fwdpp.py", "gen_fwdpp16.py", "gen_fwd8pp.py"):
         args += ["--out", str(out)]
         subprocess.run(args, check=True, capture_output=True)
     else:
@@ -30,7 +32,7 @@ def test_generated_body_matches_generator(tmp_path, gen, body):
 
 
 @pytest.mark.parametrize("body", ["fmha_fwd4_body.h", "fmha_fwd8_body.h", "fmha_fwdpp_body.h",
-                                  "fmha_fwd8pp_body.h"])
+                                  "fmha_fwdpp16_body.h", "fmha_fwd8pp_body.h"])
 def test_return_addresses_guarded(body):
     """Every s_getpc_b64 return address in the generated bodies has an assembler guard that pins
     the sign of its offset (the redo fault of round 4 came from a stub moved

@@ -1,27 +1,82 @@
-"""GPU: the generated D = 128 forward kernels the knobs select, in the default run.
+"""GPU: the generated D = 128 forward kernels the knobs select.
 
-fwd_w4 = 1 (4-wave, csrc/fmha_fwd4_kernel.h) and 2 (8-wave ping-pong, csrc/fmha_fwdpp_kernel.h,
-the default); fp8_w4 = 1 (4-wave fp8, the default) and 2 (ping-pong fp8,
-csrc/fmha_fwd8pp_kernel.h).  Each setting runs the same cases: the kernel id is asserted
-(fmha_last_kernel), the output is held to the oracle by the reference's rule (test.py:975), and
-the two kernels of a pair must agree bit for bit - they compute every row with the same tile
-order, reference max and operation order, only the row-to-wave split and the schedule differ.
-(The whole GPU suite also runs under each non-default value: profiles/r05_knob_suite.log.)
+fwd_w4 = 1 (4-wave, csrc/fmha_fwd4_kernel.h), 2 (8-wave ping-pong, csrc/fmha_fwdpp_kernel.h)
+and 3 (the ping-pong on v_mfma_f32_16x16x32, tools/gen_fwdpp16.py; 4 = auto, the default, picks
+3 or 2 by mask); fp8_w4 = 1 (4-wave fp8, the default) and 2 (ping-pong fp8,
+csrc/fmha_fwd8pp_kernel.h).  The kernels no default path runs (fwd_w4 = 1, fp8_w4 = 2) live only
+in the variants build (lib/variants/libpaged-attention.so, build.py: XFA_VARIANTS=1), which these
+tests load next to the product library through the same C ABI.  Each setting runs the same
+cases: the kernel id is asserted (fmha_last_kernel), the output is held to the oracle by the
+reference's rule (test.py:975), and the two kernels of a pair must agree bit for bit - they
+compute every row with the same tile order, reference max and operation order, only the
+row-to-wave split and the schedule differ.  The 16x16x32 ping-pong sums each MFMA's products in
+another order, so it is held to the oracle (O) and to the 32x32x16 kernel's LSE within 1e-4.
 """
 import pytest
 import torch
 
 from oracle import attention_ref as orc
-from tests import test_fp8_gpu as f8
 from tests import test_fwd4_redo_gpu as r4
 
 pytestmark = pytest.mark.gpu
+DEV = "cuda"
 
 
 @pytest.fixture(scope="module")
 def xfa():
     import xf_flash_attention_cutlass_amd as m
     return m
+
+
+_VAR = {}
+
+
+def _variants():
+    """the variants build, loaded once (ctypes; its soname differs from the product's)"""
+    if "lib" not in _VAR:
+        from xf_flash_attention_cutlass_amd import capi
+        _VAR["lib"] = capi.load(capi.VARIANTS_PATH)
+    return _VAR["lib"]
+
+
+def _run(lib, fn):
+    from xf_flash_attention_cutlass_amd import capi
+    fn()
+    if lib.fmha_last_status() != 0:
+        raise RuntimeError(lib.fmha_last_error().decode())
+    torch.cuda.synchronize()
+    return lib.fmha_last_kernel().decode()
+
+
+def _fwd_lib(lib, w4, q, k, v, causal, window=(-1, -1)):
+    """fmha_fwd of `lib` with fwd_w4 = w4, one split: (O, LSE); asserts the kernel that ran"""
+    from xf_flash_attention_cutlass_amd import capi
+    b, sq, h, d = q.shape
+    sk, hk = k.shape[1], k.shape[2]
+    q, k, v = (x.to(DEV).contiguous() for x in (q, k, v))
+    o = torch.empty_like(q)
+    lse = torch.empty(b, h, sq, device=DEV, dtype=torch.float32)
+    wl, wr = (-1, 0) if causal else window
+    old = lib.fmha_get_option(b"fwd_w4")
+    assert lib.fmha_set_option(b"fwd_w4", w4) == 0, lib.fmha_last_error()
+    try:
+        kern = _run(lib, lambda: lib.fmha_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), None, sq, sk,
+                                              b, h, hk, d, 0.0, capi.stream_handle(), None, d ** -0.5, None,
+                                              lse.data_ptr(), wl, wr, 0.0, False, q.dtype == torch.float16, 1))
+    finally:
+        lib.fmha_set_option(b"fwd_w4", old)
+    assert kern.startswith(r4.expected_kernel(w4, wr) + " "), kern
+    return o.cpu(), lse.cpu()
+
+
+def test_product_refuses_variant_kernels():
+    """the product library has no fwd_w4 = 1 / fp8_w4 = 2 kernels and says so"""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    assert L.fmha_set_option(b"fwd_w4", 1) != 0 and b"variants" in L.fmha_last_error()
+    assert L.fmha_set_option(b"fp8_w4", 2) != 0 and b"variants" in L.fmha_last_error()
+    V = _variants()
+    assert b"variants" in V.fmha_version()
 
 
 BF16_CASES = [
@@ -33,22 +88,27 @@ BF16_CASES = [
 ]
 
 
+def _pair(q, k, v, causal, window):
+    """4-wave (variants) vs ping-pong (variants and product): oracle + bit identity"""
+    from xf_flash_attention_cutlass_amd import capi
+    o1 = _fwd_lib(_variants(), 1, q, k, v, causal, window)
+    o2 = _fwd_lib(_variants(), 2, q, k, v, causal, window)
+    o2p = _fwd_lib(capi.lib(), 2, q, k, v, causal, window)
+    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
+    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
+    ok, err, bound = orc.parity_ok(o2[0].float(), ref, pt, 2.0, 1e-5)
+    assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
+    for x, y in ((o1, o2), (o2, o2p)):
+        assert torch.equal(x[0], y[0]) and torch.equal(x[1], y[1])
+
+
 @pytest.mark.parametrize("b,h,hk,sq,sk,causal,window", BF16_CASES)
 def test_fwd_w4_kernels_agree(b, h, hk, sq, sk, causal, window):
     g = torch.Generator().manual_seed(sq + sk)
     q = torch.randn(b, sq, h, 128, generator=g).bfloat16()
     k = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
     v = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
-    outs = {}
-    for w4 in (1, 2):
-        with r4._option("fwd_w4", w4):
-            outs[w4] = r4._fwd(q, k, v, causal, window)     # asserts the kernel id for w4
-    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
-    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
-    ok, err, bound = orc.parity_ok(outs[2][0].float(), ref, pt, 2.0, 0.0)
-    assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
-    assert torch.equal(outs[1][0], outs[2][0])
-    assert torch.equal(outs[1][1], outs[2][1])
+    _pair(q, k, v, causal, window)
 
 
 FP8_CASES = [
@@ -59,13 +119,40 @@ FP8_CASES = [
 ]
 
 
+def _fp8_lib(lib, w4, b, h, hk, sq, sk, causal, seed):
+    """fmha_fwd_fp8 of `lib` with fp8_w4 = w4 (bf16 out), checked against the fp8 oracle
+    estimate (tests/test_fp8_gpu.py's rule); returns O"""
+    from xf_flash_attention_cutlass_amd import capi
+    from tests import test_fp8_gpu as f8
+    (q8, qs), (k8, ks), (v8, vs) = f8._case(b, h, hk, sq, sk, seed)
+    qd8, kd8, vd8 = (x.to(DEV) for x in (q8, k8, v8))
+    o = torch.empty(b, sq, h, 128, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(b, h, sq, device=DEV, dtype=torch.float32)
+    old = lib.fmha_get_option(b"fp8_w4")
+    assert lib.fmha_set_option(b"fp8_w4", w4) == 0, lib.fmha_last_error()
+    try:
+        kern = _run(lib, lambda: lib.fmha_fwd_fp8(qd8.data_ptr(), kd8.data_ptr(), vd8.data_ptr(), o.data_ptr(),
+                                                  lse.data_ptr(), qs, ks, vs, sq, sk, b, h, hk, 128,
+                                                  128 ** -0.5, -1, 0 if causal else -1, False,
+                                                  capi.stream_handle()))
+    finally:
+        lib.fmha_set_option(b"fp8_w4", old)
+    assert kern.startswith({1: "fmha_fwd8w_kernel ", 2: "fmha_fwd8pp_kernel "}[w4]), kern
+    qd, kd, vd = q8.float() * qs, k8.float() * ks, v8.float() * vs
+    ref, _ = orc.attention_ref(qd, kd, vd, causal=causal)
+    pt = orc.attention_fp8_pt(q8, k8, v8, qs, ks, vs, causal=causal).to(torch.bfloat16)
+    ok, err, bound = orc.parity_ok(o.cpu().float(), ref, pt, 3.0, 1e-3)
+    assert ok, f"fp8 max|out-ref|={err:.3g} > {bound:.3g}"
+    return o.cpu()
+
+
 @pytest.mark.parametrize("b,h,hk,sq,sk,causal", FP8_CASES)
-def test_fp8_w4_kernels_agree(xfa, b, h, hk, sq, sk, causal):
-    outs = {}
-    for w4 in (1, 2):
-        with r4._option("fp8_w4", w4):
-            outs[w4] = f8._check(xfa, b, h, hk, sq, sk, causal=causal, seed=sq)  # oracle + kernel id
-    assert torch.equal(outs[1], outs[2])
+def test_fp8_w4_kernels_agree(b, h, hk, sq, sk, causal):
+    from xf_flash_attention_cutlass_amd import capi
+    o1 = _fp8_lib(_variants(), 1, b, h, hk, sq, sk, causal, sq)
+    o2 = _fp8_lib(_variants(), 2, b, h, hk, sq, sk, causal, sq)
+    o1p = _fp8_lib(capi.lib(), 1, b, h, hk, sq, sk, causal, sq)
+    assert torch.equal(o1, o2) and torch.equal(o1, o1p)
 
 
 def _sweep(n, seed):
@@ -95,16 +182,7 @@ def test_fwd_w4_kernels_sweep(b, h, hk, sq, sk, causal, window, dt):
     q = torch.randn(b, sq, h, 128, generator=g).to(dt)
     k = torch.randn(b, sk, hk, 128, generator=g).to(dt)
     v = torch.randn(b, sk, hk, 128, generator=g).to(dt)
-    outs = {}
-    for w4 in (1, 2):
-        with r4._option("fwd_w4", w4):
-            outs[w4] = r4._fwd(q, k, v, causal, window)
-    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
-    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
-    ok, err, bound = orc.parity_ok(outs[2][0].float(), ref, pt, 2.0, 1e-5)
-    assert ok, f"max|out-ref| = {err:.3g} > {bound:.3g}"
-    assert torch.equal(outs[1][0], outs[2][0])
-    assert torch.equal(outs[1][1], outs[2][1])
+    _pair(q, k, v, causal, window)
 
 
 def _sweep8(n, seed):
@@ -119,9 +197,106 @@ def _sweep8(n, seed):
 
 
 @pytest.mark.parametrize("b,h,hk,sq,sk,causal", _sweep8(10, 11))
-def test_fp8_w4_kernels_sweep(xfa, b, h, hk, sq, sk, causal):
-    outs = {}
-    for w4 in (1, 2):
-        with r4._option("fp8_w4", w4):
-            outs[w4] = f8._check(xfa, b, h, hk, sq, sk, causal=causal, seed=sk)
-    assert torch.equal(outs[1], outs[2])
+def test_fp8_w4_kernels_sweep(b, h, hk, sq, sk, causal):
+    o1 = _fp8_lib(_variants(), 1, b, h, hk, sq, sk, causal, sk)
+    o2 = _fp8_lib(_variants(), 2, b, h, hk, sq, sk, causal, sk)
+    assert torch.equal(o1, o2)
+
+
+def _check16(q, k, v, causal, window):
+    """fwd_w4 = 3 against the oracle (O, reference rule) and the fwd_w4 = 2 LSE; returns (O, LSE)"""
+    from xf_flash_attention_cutlass_amd import capi
+    outs = {w4: _fwd_lib(capi.lib(), w4, q, k, v, causal, window) for w4 in (2, 3, 4)}
+    assert torch.equal(outs[4][0], outs[3 if window[1] < 0 and not causal else 2][0])
+    ref, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window)
+    pt, _ = orc.attention_ref(q, k, v, causal=causal, window_size=window, upcast=False, reorder_ops=True)
+    ok, err, bound = orc.parity_ok(outs[3][0].float(), ref, pt, 2.0, 1e-5)
+    assert ok, f"16x16: max|out-ref| = {err:.3g} > {bound:.3g}"
+    l2, l3 = outs[2][1], outs[3][1]
+    assert torch.equal(torch.isinf(l2), torch.isinf(l3))
+    fin = torch.isfinite(l2)
+    assert (l2[fin] - l3[fin]).abs().max().item() <= 1e-4
+    return outs[3]
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal,window", BF16_CASES)
+def test_fwd_w4_16x16_cases(b, h, hk, sq, sk, causal, window):
+    g = torch.Generator().manual_seed(sq + sk)
+    q = torch.randn(b, sq, h, 128, generator=g).bfloat16()
+    k = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
+    v = torch.randn(b, sk, hk, 128, generator=g).bfloat16()
+    _check16(q, k, v, causal, window)
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal,window,dt", _sweep(20, 5) + _sweep(12, 23))
+def test_fwd_w4_16x16_sweep(b, h, hk, sq, sk, causal, window, dt):
+    g = torch.Generator().manual_seed(b * 1000 + sq * 7 + sk)
+    q = torch.randn(b, sq, h, 128, generator=g).to(dt)
+    k = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    v = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    _check16(q, k, v, causal, window)
+
+
+@pytest.mark.parametrize("opts", [(("fwd_persistent", 1), ("fwd_order", 0)),
+                                  (("fwd_persistent", 1), ("fwd_order", 1)),
+                                  (("fwd_persistent", 1), ("fwd_dyn", 2))])
+def test_fwd_w4_multi_item_schedules(opts):
+    """more items than CUs (4 x 16 heads x 8 row blocks = 512 items), so each persistent
+    workgroup reuses its LDS ring across items: the 4-wave and ping-pong kernels stay bit
+    identical under every schedule, the 16x16x32 one meets the oracle on samples"""
+    V = _variants()
+    g = torch.Generator().manual_seed(99)
+    b, h, s = 4, 16, 2048
+    q = torch.randn(b, s, h, 128, generator=g).bfloat16()
+    k = torch.randn(b, s, h, 128, generator=g).bfloat16()
+    v = torch.randn(b, s, h, 128, generator=g).bfloat16()
+    olds = {n: V.fmha_get_option(n.encode()) for n, _ in opts}
+    try:
+        for n, val in opts:
+            assert V.fmha_set_option(n.encode(), val) == 0
+        o1 = _fwd_lib(V, 1, q, k, v, True)
+        o2 = _fwd_lib(V, 2, q, k, v, True)
+        o3 = _fwd_lib(V, 3, q, k, v, False)
+    finally:
+        for n, val in olds.items():
+            V.fmha_set_option(n.encode(), val)
+    assert torch.equal(o1[0], o2[0]) and torch.equal(o1[1], o2[1])
+    for bb, hh in ((0, 0), (3, 15)):
+        qs, ks, vs = (x[bb:bb + 1, :, hh:hh + 1] for x in (q, k, v))
+        ref, _ = orc.attention_ref(qs, ks, vs, causal=False)
+        pt, _ = orc.attention_ref(qs, ks, vs, causal=False, upcast=False, reorder_ops=True)
+        ok, err, bound = orc.parity_ok(o3[0][bb:bb + 1, :, hh:hh + 1].float(), ref, pt, 2.0, 1e-5)
+        assert ok, f"16x16 multi-item ({bb}, {hh}): {err:.3g} > {bound:.3g}"
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_fwdpp_varlen_seqused_k(xfa, causal):
+    """varlen with seqused_k (each sequence reads only the first seqused_k[b] of its keys, the
+    non-paged per-sequence key limit of flash-attn's varlen path): that route into the
+    ping-pong kernels, against the oracle per sequence"""
+    from xf_flash_attention_cutlass_amd import capi
+    pa = xfa.paged_attn
+    g = torch.Generator().manual_seed(123)
+    h, hk = 8, 4
+    lq, lk, used = [300, 129, 500], [1000, 300, 777], [1000, 17, 600]
+    cq = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32)
+    ck = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32)
+    q = torch.randn(int(cq[-1]), h, 128, generator=g).bfloat16()
+    k = torch.randn(int(ck[-1]), hk, 128, generator=g).bfloat16()
+    v = torch.randn(int(ck[-1]), hk, 128, generator=g).bfloat16()
+    r = pa.varlen_fwd(q.to(DEV), k.to(DEV), v.to(DEV), None, cq.to(DEV), ck.to(DEV),
+                      torch.tensor(used, dtype=torch.int32, device=DEV), None, None, max(lq), max(lk),
+                      0.0, 128 ** -0.5, False, causal, -1, -1, 0.0, False, None)
+    torch.cuda.synchronize()
+    out = r[0].cpu()
+    kern = capi.lib().fmha_last_kernel().decode()
+    assert kern.startswith(r4.expected_kernel(capi.lib().fmha_get_option(b"fwd_w4"),
+                                              0 if causal else -1) + " "), kern
+    for i in range(len(lq)):
+        a_, b_ = int(cq[i]), int(cq[i + 1])
+        c_ = int(ck[i])
+        qs, ks, vs = q[a_:b_][None], k[c_:c_ + used[i]][None], v[c_:c_ + used[i]][None]
+        ref, _ = orc.attention_ref(qs, ks, vs, causal=causal)
+        pt, _ = orc.attention_ref(qs, ks, vs, causal=causal, upcast=False, reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[a_:b_][None].float(), ref, pt, 2.0, 1e-5)
+        assert ok, f"seqused_k seq {i}: {err:.3g} > {bound:.3g}"

@@ -77,7 +77,8 @@ def _cus(L):
 def test_deterministic_bwd_workspace_bounded():
     """deterministic=True: S = min(ceil(CUs / (b * hk)), key blocks) dQ slices (export.cpp:1090-1091's
     bound; no workgroup walks more slices than there are 256-key blocks), capped at 8 GiB of
-    slices beyond the first, so the workspace stops growing with seqlen_k."""
+    slices beyond the first, so the workspace stops growing with seqlen_k.  Beside the
+    slices: D = rowsum(dO O) and the causal-ALiBi LSE in the kernels' convention, fp32 per row."""
     L = capi.lib()
     cus = _cus(L)
     assert cus >= 1
@@ -87,17 +88,17 @@ def test_deterministic_bwd_workspace_bounded():
         for sk in (128, 4096, 65536, 1 << 20):
             nkb = -(-sk // 256)
             slices = min(-(-cus // (b * hk)), nkb, 1 + (8 << 30) // _acc(tok, h))
-            want = slices * _acc(tok, h) + _dsum(tok, h)
+            want = slices * _acc(tok, h) + 2 * _dsum(tok, h)
             assert L.fmha_bwd_workspace_size(sq, sk, b, h, hk, 128, True) == want, (b, h, hk, sq, sk)
             assert L.fmha_varlen_bwd_workspace_size(tok, sk, b, h, hk, 128, True) == want
-        assert L.fmha_bwd_workspace_size(sq, 4096, b, h, hk, 128, False) == _acc(tok, h) + _dsum(tok, h)
+        assert L.fmha_bwd_workspace_size(sq, 4096, b, h, hk, 128, False) == _acc(tok, h) + 2 * _dsum(tok, h)
     # MQA, one sequence of 32k tokens x 64 query heads (1 GiB per slice): the byte cap bounds it
     # (the CU bound alone asked for 256 slices = 256 GiB)
     ws = L.fmha_bwd_workspace_size(32768, 32768, 1, 64, 1, 128, True)
-    assert ws <= 9 * _acc(32768, 64) + _dsum(32768, 64)
+    assert ws <= 9 * _acc(32768, 64) + 2 * _dsum(32768, 64)
     # B4 H32 S16384 D128: at most two slices on a 256-CU device
     assert L.fmha_bwd_workspace_size(16384, 16384, 4, 32, 32, 128, True) <= (
-        max(2, -(-cus // 128)) * _acc(4 * 16384, 32) + _dsum(4 * 16384, 32))
+        max(2, -(-cus // 128)) * _acc(4 * 16384, 32) + 2 * _dsum(4 * 16384, 32))
 
 
 @pytest.mark.parametrize("kw", [dict(dropout_p=0.1), dict(softcap=30.0),

@@ -45,6 +45,8 @@ def main():
 
 def run(a, mon):
     import torch
+    import bench
+    mon.select(bench.device_info(torch.device("cuda", 0))["pci_bus"])
     from xf_flash_attention_cutlass_amd import capi
     B, S, H, D = 4, 4096, 32, 128
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -85,7 +87,8 @@ def run(a, mon):
         def f():
             assert lib.pp_launch(P(q), P(k), P(v), P(po), P(plse), B, S, H, H, sc, full, stream) == 0
         return f
-    variants.append((f"pp skel {pps[0][0]} (MFMA+LDS+DMA+barriers) [INVALID]", pp_run(pps[0][1], 0)))
+    for name, lib in pps:
+        variants.append((f"pp skel {name} (MFMA+LDS+DMA+barriers) [INVALID]", pp_run(lib, 0)))
     for name, lib in pps:
         variants.append((f"pp full {name} (8-wave ping-pong)", pp_run(lib, 1)))
 

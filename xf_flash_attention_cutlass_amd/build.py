@@ -7,7 +7,12 @@ Produces
   xf_flash_attention_cutlass_amd/lib/paged_attn*.so          — the pybind/ATen module
       `paged_attn` (export.cpp equivalent), linked against libpaged-attention.so.
 
-Usage: python xf_flash_attention_cutlass_amd/build.py [--no-ext] [-j N] [--force]
+  xf_flash_attention_cutlass_amd/lib/variants/libpaged-attention.so — the same C ABI built with
+      XFA_VARIANTS=1: also the kernels no default path runs (the 4-wave D = 128 forward, fwd_w4
+      = 1; the ping-pong fp8 forward, fp8_w4 = 2), for A/B runs and the bit-identity tests
+      (tests/test_kernel_variants_gpu.py); the product library refuses those option values.
+
+Usage: python xf_flash_attention_cutlass_amd/build.py [--no-ext] [--no-variants] [-j N] [--force]
 """
 from __future__ import annotations
 
@@ -61,8 +66,15 @@ def _compile(job):
     return out, None
 
 
-def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+VARIANT_TUS = {"fmha_fwd_hd128_bf16.o", "fmha_fwd_hd128_f16.o", "fmha_fwd_fp8.o", "fmha_api.o"}
+VARIANTS_DIR = os.path.join(LIB, "variants")
+
+
+def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False, variants: bool = False) -> str:
+    """variants: lib/variants/libpaged-attention.so; the translation units XFA_VARIANTS changes
+    are rebuilt with it (into lib/obj_variants), the others shared with the product build."""
+    obj_dir = os.path.join(LIB, "obj_variants") if variants else OBJ
+    os.makedirs(obj_dir, exist_ok=True)
     todo = []
     for hd, dt in VARIANTS:
         defs = [f"-DXFA_HD={hd}", f"-DXFA_DTN={dt}", f"-DXFA_DT_BF16={1 if dt == 'bf16' else 0}"]
@@ -72,13 +84,18 @@ def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     todo.append((os.path.join(CSRC, "fmha_append.hip"), os.path.join(OBJ, "fmha_append.o"), []))
     todo.append((os.path.join(CSRC, "fmha_fwd_fp8.hip"), os.path.join(OBJ, "fmha_fwd_fp8.o"), []))
     todo.append((os.path.join(CSRC, "fmha_api.cpp"), os.path.join(OBJ, "fmha_api.o"), []))
+    if variants:
+        todo = [(src, os.path.join(obj_dir, os.path.basename(out)), defs + ["-DXFA_VARIANTS=1"])
+                for src, out, defs in todo if os.path.basename(out) in VARIANT_TUS]
+        todo += [(None, os.path.join(OBJ, n), None) for n in sorted(os.listdir(OBJ))
+                 if n.endswith(".o") and n not in VARIANT_TUS]
     if force:
-        for _, out, _ in todo:
-            if os.path.exists(out):
+        for src, out, _ in todo:
+            if src and os.path.exists(out):
                 os.remove(out)
     errors = []
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        for out, err in ex.map(_compile, todo):
+        for out, err in ex.map(_compile, [t for t in todo if t[0]]):
             if err:
                 errors.append(err)
             elif verbose:
@@ -86,10 +103,13 @@ def build_lib(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
     objs = [o for _, o, _ in todo]
-    so = os.path.join(LIB, LIBNAME)
+    if variants:
+        os.makedirs(VARIANTS_DIR, exist_ok=True)
+    so = os.path.join(VARIANTS_DIR if variants else LIB, LIBNAME)
+    soname = "libpaged-attention-variants.so" if variants else LIBNAME
     if not _newer(so, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so, *objs,
-               "-Wl,-soname," + LIBNAME]
+               "-Wl,-soname," + soname]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -154,10 +174,13 @@ def main(argv=None):
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-ext", action="store_true")
+    ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     so = build_lib(a.jobs, a.force, a.verbose)
     print("built", so)
+    if not a.no_variants:
+        print("built", build_lib(a.jobs, a.force, a.verbose, variants=True))
     print("built", build_c_smoke(a.force))
     if not a.no_ext:
         print("built", build_ext(a.force, a.verbose))

@@ -12,6 +12,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libpaged-attention.so")
+# the same C ABI with the non-default kernels compiled in (build.py: XFA_VARIANTS=1), for A/B
+# runs and the bit-identity tests only
+VARIANTS_PATH = os.path.join(_HERE, "lib", "variants", "libpaged-attention.so")
 
 vp, i32, f32, b_, sz = C.c_void_p, C.c_int32, C.c_float, C.c_bool, C.c_size_t
 

@@ -200,9 +200,29 @@ void set_scales(FwdParams& p, float softmax_scale, float softcap) {
 }
 
 // Window normalisation (paged_attn.cpp:116-120): causal <=> wl < 0 && wr == 0.
-void set_windows(int& wl, int& wr, int seqlen_k) {
+template <typename P>
+static LseAlibiParams lse_alibi_params(const P& p, float sign) {
+    LseAlibiParams a{};
+    a.src = p.lse; a.dst = nullptr; a.sign = sign;
+    a.alibi = p.alibi; a.alibi_bstride = p.alibi_bstride;
+    a.b = p.b; a.h = p.h; a.seqlen_q = p.seqlen_q; a.seqlen_k = p.seqlen_k;
+    a.cu_seqlens_q = p.cu_seqlens_q; a.cu_seqlens_k = p.cu_seqlens_k;
+    a.lse_batch = p.lse_batch; a.lse_head = p.lse_head;
+    return a;
+}
+static LseAlibiParams lse_alibi_params(const FwdParams& p, float sign) {
+    LseAlibiParams a = lse_alibi_params<FwdParams>(p, sign);
+    a.dst = p.lse;
+    a.seqused_k = p.seqused_k; a.leftpad_k = p.leftpad_k;
+    return a;
+}
+
+// Returns the reference's is_causal (before the normalisation), which picks its ALiBi form.
+bool set_windows(int& wl, int& wr, int seqlen_k) {
+    const bool causal = wl < 0 && wr == 0;
     if (wl < 0 && wr >= 0) wl = seqlen_k;
     if (wl >= 0 && wr < 0) wr = seqlen_k;
+    return causal;
 }
 
 bool check_common(const void* q, const void* k, const void* v, const void* o, int b, int h,
@@ -347,7 +367,9 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
         p.work_ctr = counter_get(st);
         if (!p.work_ctr) { fail(3, "could not allocate the item-queue counters"); return; }
     }
-    hip_ok(dispatch_fwd(p, bf16, st), "forward launch");
+    if (!hip_ok(dispatch_fwd(p, bf16, st), "forward launch")) return;
+    // causal ALiBi: the LSE in the reference's convention (+slope key, mask_hip.h:163-164)
+    if (p.lse && p.alibi && p.alibi_causal) hip_ok(launch_lse_alibi(lse_alibi_params(p, +1.f), st), "LSE ALiBi pass");
 }
 
 }  // namespace
@@ -358,7 +380,7 @@ const char* fmha_last_error(void) { return g_err.c_str(); }
 int fmha_last_status(void) { return g_status; }
 int fmha_last_num_splits(void) { return g_last_splits; }
 const char* fmha_last_kernel(void) { return g_last_kernel; }
-const char* fmha_version(void) { return "xf-fmha-gfx950 2.3"; }
+const char* fmha_version(void) { return XFA_VARIANTS ? "xf-fmha-gfx950 2.4 (variants)" : "xf-fmha-gfx950 2.4"; }
 
 void fmha_set_rng_state(uint64_t seed, uint64_t offset) {
     g_seed = seed;
@@ -387,7 +409,7 @@ int fmha_set_option(const char* name, int value) {
         {"fwd_xcdq", &o.fwd_xcdq, 0, 1},         {"fwd_pipe", &o.fwd_pipe, 0, 2},
         {"fwd_decode", &o.fwd_decode, 0, 1},     {"dec_wg_per_cu", &o.dec_wg_per_cu, 1, 16},
         {"dec_hmaj", &o.dec_hmaj, 0, 2},
-        {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 2},
+        {"dec_mr", &o.dec_mr, 16, 32},           {"fwd_w4", &o.fwd_w4, 0, 4},
         {"bwd_order", &o.bwd_order, 0, 1},       {"bwd_desc", &o.bwd_desc, 0, 1},
         {"dec_fold", &o.dec_fold, 0, 1},        {"dec_bal", &o.dec_bal, 0, 1},
         {"fp8_w4", &o.fp8_w4, 0, 2},           {"comb_row", &o.comb_row, 0, 1},
@@ -397,6 +419,11 @@ int fmha_set_option(const char* name, int value) {
         if (value < k.lo || value > k.hi || (k.slot == &o.fwd_waves && value != 4 && value != 8) ||
             (k.slot == &o.dec_mr && value != 16 && value != 32)) {
             fail(1, "option %s: value %d out of range [%d, %d]", name, value, k.lo, k.hi);
+            return -1;
+        }
+        if (!XFA_VARIANTS && ((k.slot == &o.fwd_w4 && value == 1) || (k.slot == &o.fp8_w4 && value == 2))) {
+            fail(1, "option %s = %d selects a kernel only the variants build has "
+                    "(lib/variants/libpaged-attention.so, build.py --variants)", name, value);
             return -1;
         }
         k.slot->store(value);
@@ -443,7 +470,7 @@ void fmha_fwd(void* q_ptr, void* k_ptr, void* v_ptr, void* o_ptr, void* alibi_sl
         dense_strides(p, seqlen_q, seqlen_k, num_heads, num_heads_k, head_size);
         p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
         p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
-        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.alibi_causal = set_windows(window_size_left, window_size_right, seqlen_k);
         p.wl = window_size_left; p.wr = window_size_right;
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes_ptr;
@@ -497,7 +524,7 @@ void fmha_fwd_strided(void* q, void* k, void* v, void* o, void* alibi_slopes, vo
         p.lse_batch = (int64_t)num_heads * seqlen_q; p.lse_head = seqlen_q;
         p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
         p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
-        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.alibi_causal = set_windows(window_size_left, window_size_right, seqlen_k);
         p.wl = window_size_left; p.wr = window_size_right;
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes;
@@ -532,7 +559,7 @@ void fmha_fwd_fp8(void* q, void* k, void* v, void* o, void* softmax_lse, float q
         dense_strides(p, seqlen_q, seqlen_k, num_heads, num_heads_k, head_size);
         p.b = batch_size; p.h = num_heads; p.hk = num_heads_k; p.group = num_heads / num_heads_k;
         p.d = head_size; p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
-        set_windows(window_size_left, window_size_right, seqlen_k);
+        p.alibi_causal = set_windows(window_size_left, window_size_right, seqlen_k);
         p.wl = window_size_left; p.wr = window_size_right;
         set_scales(p, softmax_scale, 0.f);
         p.q_scale = q_scale; p.k_scale = k_scale; p.v_scale = v_scale;
@@ -602,7 +629,7 @@ void fmha_varlen_fwd_ex(void* q, void* k, void* v, void* o, void* softmax_lse,
         p.seqused_k = (const int*)seqused_k;
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
-        set_windows(window_size_left, window_size_right, max_seqlen_k);
+        p.alibi_causal = set_windows(window_size_left, window_size_right, max_seqlen_k);
         p.wl = window_size_left; p.wr = window_size_right;
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes; p.alibi_bstride = alibi_batch_stride;
@@ -671,7 +698,7 @@ void fmha_page_kvcache_fwd_ex(void* q, void* kcache, void* vcache, void* o, void
         p.leftpad_k = (const int*)cache_leftpad;
         p.b = batch_size; p.h = h; p.hk = hk; p.group = h / hk; p.d = d;
         p.seqlen_q = seqlen_q; p.seqlen_k = max_seqlen_k;
-        set_windows(window_size_left, window_size_right, max_seqlen_k);
+        p.alibi_causal = set_windows(window_size_left, window_size_right, max_seqlen_k);
         p.wl = window_size_left; p.wr = window_size_right;
         set_scales(p, softmax_scale, softcap);
         p.alibi = (const float*)alibi_slopes; p.alibi_bstride = alibi_batch_stride;
@@ -776,12 +803,23 @@ static int bwd_slices(int64_t tokens, int batch, int h, int hk, int d, int seqle
     s = (int)std::min<size_t>((size_t)s, 1 + kDetSliceCap / acc);
     return std::max(1, s);
 }
+// workspace: [dQ slices][D = rowsum(dO O)][lse_fix: the causal-ALiBi LSE in the kernels' form]
 static size_t bwd_ws_bytes(int64_t tokens, int h, int d, int slices) {
-    return (size_t)slices * bwd_acc_bytes(tokens, h, d) + bwd_dsum_bytes(tokens, h);
+    return (size_t)slices * bwd_acc_bytes(tokens, h, d) + 2 * bwd_dsum_bytes(tokens, h);
+}
+// causal ALiBi: softmax_lse (the reference's convention) -> lse_fix in the kernels' own, which
+// the backward then reads
+static bool bwd_lse_convention(BwdParams& p, hipStream_t st) {
+    if (!(p.alibi && p.alibi_causal)) return true;
+    LseAlibiParams a = lse_alibi_params(p, -1.f);
+    a.dst = p.lse_fix;
+    if (!hip_ok(launch_lse_alibi(a, st), "LSE ALiBi pass")) return false;
+    p.lse = p.lse_fix;
+    return true;
 }
 // slices a caller's workspace of `bytes` holds (0 if not even one)
 static int bwd_slices_fit(int64_t tokens, int h, int d, size_t bytes) {
-    const size_t fixed = bwd_dsum_bytes(tokens, h), acc = std::max<size_t>(1, bwd_acc_bytes(tokens, h, d));
+    const size_t fixed = 2 * bwd_dsum_bytes(tokens, h), acc = std::max<size_t>(1, bwd_acc_bytes(tokens, h, d));
     return bytes < fixed ? 0 : (int)std::min<size_t>((bytes - fixed) / acc, 1 << 20);
 }
 
@@ -809,7 +847,7 @@ static bool bwd_rows_ok(int64_t tokens, int h, int d) {
 
 static bool bwd_common(BwdParams& p, float softmax_scale, float softcap, int wl, int wr,
                        int seqlen_k_norm) {
-    set_windows(wl, wr, seqlen_k_norm);
+    p.alibi_causal = set_windows(wl, wr, seqlen_k_norm);
     p.wl = wl; p.wr = wr;
     float scale_softmax = softmax_scale;
     p.softcap_on = softcap > 0.f;
@@ -860,6 +898,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes((int64_t)batch_size * seqlen_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
+        p.lse_fix = (float*)(ws + slices * acc + bwd_dsum_bytes((int64_t)batch_size * seqlen_q, h));
         p.dq_slices = deterministic ? slices : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = (int64_t)seqlen_q * h * d;
@@ -878,6 +917,7 @@ void fmha_bwd(void* dout, void* q, void* k, void* v, void* out, void* softmax_ls
         p.seqlen_q = seqlen_q; p.seqlen_k = seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, seqlen_k);
         if (!set_dropout(p, p_dropout, softcap)) return;
+        if (!bwd_lse_convention(p, stream)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_bwd");
@@ -925,6 +965,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.dq_accum = (float*)ws;
         const size_t acc = bwd_acc_bytes(total_q, h, d);
         p.dsum = softmax_d ? (float*)softmax_d : (float*)(ws + slices * acc);
+        p.lse_fix = (float*)(ws + slices * acc + bwd_dsum_bytes(total_q, h));
         p.dq_slices = deterministic ? slices : 0;   // slices a workgroup walks into
         p.acc_slice = (int64_t)(acc / sizeof(float));
         p.q_row = (int64_t)h * d; p.q_head = d; p.q_batch = 0;
@@ -945,6 +986,7 @@ void fmha_varlen_bwd(void* dout, void* q, void* k, void* v, void* out, void* sof
         p.seqlen_q = max_seqlen_q; p.seqlen_k = max_seqlen_k;
         bwd_common(p, softmax_scale, softcap, window_size_left, window_size_right, max_seqlen_k);
         if (!set_dropout(p, p_dropout, softcap)) return;
+        if (!bwd_lse_convention(p, stream)) return;
         hip_ok(dispatch_bwd(p, !is_fp16, stream), "varlen backward launch");
     } catch (...) {
         fail(9, "internal error in fmha_varlen_bwd");

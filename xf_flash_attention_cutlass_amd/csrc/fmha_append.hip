@@ -137,4 +137,28 @@ hipError_t launch_append(const AppendParams& p, bool fp16, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- causal ALiBi LSE ------
+__global__ void __launch_bounds__(256) fmha_lse_alibi_kernel(const LseAlibiParams p) {
+    const int bh = blockIdx.x;
+    const int bidx = bh / p.h, head = bh - bidx * p.h;
+    int q_off = 0, sq = p.seqlen_q, sk = p.seqlen_k;
+    if (p.cu_seqlens_q) { q_off = p.cu_seqlens_q[bidx]; sq = p.cu_seqlens_q[bidx + 1] - q_off; }
+    if (p.cu_seqlens_k) sk = p.cu_seqlens_k[bidx + 1] - p.cu_seqlens_k[bidx];
+    if (p.seqused_k) sk = p.seqused_k[bidx];
+    if (p.leftpad_k) sk -= p.leftpad_k[bidx];
+    const int pos = blockIdx.y * 256 + threadIdx.x;
+    if (pos >= sq) return;
+    const float slope = p.alibi[bidx * p.alibi_bstride + head];
+    const int64_t i = (int64_t)bidx * p.lse_batch + (int64_t)head * p.lse_head + q_off + pos;
+    const float x = p.src[i];
+    p.dst[i] = isfinite(x) ? x + p.sign * slope * (float)(pos + sk - sq) : x;
+}
+
+hipError_t launch_lse_alibi(const LseAlibiParams& p, hipStream_t st) {
+    const int max_sq = p.seqlen_q;     // (varlen: max_seqlen_q)
+    if (max_sq <= 0 || p.b * p.h <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fmha_lse_alibi_kernel, dim3(p.b * p.h, (max_sq + 255) / 256), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
 }  // namespace xfa

@@ -117,6 +117,7 @@ struct FwdParams {
     float softcap_pre;         // >0: w = tanh(s * softcap_pre)
     float alibi_mul;           // 1 / scale_softmax (bias in working units)
     int num_splits;
+    int alibi_causal;          // the reference's is_causal with ALiBi: its LSE convention differs
     int kv_fp8;                // 1: K/V stored as fp8 e4m3fn
     float k_scale, v_scale;    // fp8 K/V dequant scales (stored value x scale)
     float q_scale;             // fp8 Q dequant scale (fp8 Q/K/V forward)
@@ -202,6 +203,8 @@ struct BwdParams {
     float scale_log2;
     float softcap_pre;
     float alibi_mul;
+    int alibi_causal;    // causal ALiBi: the main kernel reads lse_fix (launch_lse_alibi)
+    float* lse_fix;      // workspace [like lse]: the LSE back in the kernels' ALiBi convention
     int softcap_on;
     int dq_slices;       // deterministic: dQ partials per key block in dq_accum slices (0 = atomics)
     int64_t acc_slice;   // floats between dq_accum slices

@@ -4,7 +4,9 @@
 // perturb each other's register allocation, cdna_hip_programming.md §5.4 rule 19).
 #include "fmha_fwd_kernel.h"
 #if XFA_HD == 128
-#include "fmha_fwd4_kernel.h"
+#if XFA_VARIANTS && XFA_HD == 128
+#include "fmha_fwd4_kernel.h"     // (fwd_w4 = 1: the variants build only, build.py --variants)
+#endif
 #include "fmha_fwdpp_kernel.h"
 #endif
 #include "fmha_decode_kernel.h"
@@ -156,15 +158,26 @@ static hipError_t launch_fwdpp(const FwdParams& p, hipStream_t st) {
         grid = dim3(slots, 1, 1);
     }
     constexpr bool BF = std::is_same<elem_t, __bf16>::value;
+    // fwd_w4 = 3: the body on the 16x16x32 MFMA shape (tools/gen_fwdpp16.py); 4 (auto, the
+    // default): 16x16x32 where no row has a right window (causal / local rows: 32x32x16), the
+    // faster of the two per mask on the same box
+    const bool m16 = p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0);
     static std::atomic<unsigned long long> attr_done{0};
-    once_per_device(attr_done, p.device, [&] { (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem); });
-    note_launch("fmha_fwdpp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
-    hipLaunchKernelGGL((fmha_fwdpp_kernel<BF>), grid, dim3(512), kFwdppSmem, st, pp);
+    once_per_device(attr_done, p.device, [&] {
+        (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);
+    });
+    note_launch(m16 ? "fmha_fwdpp16_kernel" : "fmha_fwdpp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
+    if (m16) hipLaunchKernelGGL((fmha_fwdpp_kernel<BF, true>), grid, dim3(512), kFwdppSmem, st, pp);
+    else hipLaunchKernelGGL((fmha_fwdpp_kernel<BF, false>), grid, dim3(512), kFwdppSmem, st, pp);
     return hipGetLastError();
 }
 
 static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
-    if (p.fwd4 == 2) return launch_fwdpp(p, st);
+    if (p.fwd4 >= 2) return launch_fwdpp(p, st);
+#if !XFA_VARIANTS
+    return hipErrorNotSupported;   // (fmha_set_option refuses fwd_w4 = 1 in this build)
+#else
     const int n_mb = (p.seqlen_q * p.group + kFwd4Rows - 1) / kFwd4Rows;
     FwdParams pp = p;
     pp.n_mblocks = n_mb;
@@ -183,6 +196,7 @@ static hipError_t launch_fwd4(const FwdParams& p, hipStream_t st) {
     note_launch("fmha_fwd4_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 256);
     hipLaunchKernelGGL((fmha_fwd4_kernel<BF>), grid, dim3(256), kFwd4Smem, st, pp);
     return hipGetLastError();
+#endif
 }
 #endif
 

@@ -2,7 +2,9 @@
 // bf16 or fp16 output; persistent XCD-paired grid as the bf16 forward.
 #include "fmha_fwd_fp8_kernel.h"
 #include "fmha_fwd8w_kernel.h"
-#include "fmha_fwd8pp_kernel.h"
+#if XFA_VARIANTS
+#include "fmha_fwd8pp_kernel.h"   // (fp8_w4 = 2: the variants build only, build.py --variants)
+#endif
 #include "fmha_launch.h"
 
 namespace xfa {
@@ -29,6 +31,7 @@ static hipError_t launch_fp8_w4(const FwdParams& p, hipStream_t st) {
     return hipGetLastError();
 }
 
+#if XFA_VARIANTS
 // 8-wave ping-pong fp8 forward (fmha_fwd8pp_kernel.h): the same items, schedules, eligibility
 template <bool F16>
 static hipError_t launch_fp8_pp(const FwdParams& p, hipStream_t st) {
@@ -49,6 +52,7 @@ static hipError_t launch_fp8_pp(const FwdParams& p, hipStream_t st) {
     hipLaunchKernelGGL((fmha_fwd8pp_kernel<F16>), grid, dim3(512), kFwd8ppSmem, st, pp);
     return hipGetLastError();
 }
+#endif
 
 template <typename T>
 static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
@@ -81,8 +85,10 @@ static hipError_t launch_fp8_t(const FwdParams& p, hipStream_t st) {
 }
 
 hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st) {
+#if XFA_VARIANTS
     if (p.fwd4 == 2 && p.k_row == p.v_row && (p.wl < 0 || p.wl >= p.seqlen_k))
         return out_fp16 ? launch_fp8_pp<true>(p, st) : launch_fp8_pp<false>(p, st);
+#endif
     if (p.fwd4 && p.k_row == p.v_row && (p.wl < 0 || p.wl >= p.seqlen_k))
         return out_fp16 ? launch_fp8_w4<true>(p, st) : launch_fp8_w4<false>(p, st);
     return out_fp16 ? launch_fp8_t<_Float16>(p, st) : launch_fp8_t<__bf16>(p, st);

@@ -23,6 +23,11 @@
 #else
 #include "fmha_fwdpp_body.h"
 #endif
+#ifdef XFA_FWDPP16_BODY
+#include XFA_FWDPP16_BODY
+#else
+#include "fmha_fwdpp16_body.h"  // the same schedule on v_mfma_f32_16x16x32 (tools/gen_fwdpp16.py)
+#endif
 
 namespace xfa {
 
@@ -53,8 +58,9 @@ __device__ __forceinline__ i32x4 fwdpp_srd(const void* base, uint32_t bytes) {
     return r;
 }
 
-// One (batch x kv head, 256-row query block) item.
-template <bool BF16>
+// One (batch x kv head, 256-row query block) item.  M16: the body on the 16x16x32 MFMA shape
+// (a lane holds rows l16 and 16 + l16 of its wave's 32; per-lane operands below).
+template <bool BF16, bool M16>
 __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const int bh, const int m_block XFA_PP_ACC_PARAM) {
     constexpr int HD = 128;
     int tid = threadIdx.x;
@@ -161,6 +167,47 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int kdst = __builtin_amdgcn_readfirstlane(sbase + wave * 2048);
     const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);
     const float thr = __builtin_amdgcn_exp2f(p.max_slack);
+    if constexpr (M16) {
+        static_assert(kFwdpp16Ring == kFwdppRing, "both bodies address the same LDS ring");
+        // row tile rt of this lane: row wrow0 + 16 rt + l16, 4 keys per 16-key block from 4 g
+        const int g = lane >> 4, l16 = lane & 15;
+        int qo[2], oo[2], lo[2], li[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int rrow = wrow0 + 16 * rt + l16;
+            const bool rok = rrow < rows_total;
+            const int rpos = rok ? rrow / G : 0;
+            const int rhead = hk_i * G + (rok ? rrow - rpos * G : 0);
+            qo[rt] = rok ? (rpos * (int)p.q_row + rhead * (int)p.q_head) * 2 + 16 * g : kOOB;  // chunk 4 s + g
+            oo[rt] = rok ? (rpos * (int)p.o_row + rhead * (int)p.o_head) * 2 + 8 * g : kOOB;   // d 16 dt + 4 g
+            lo[rt] = (rok && g == 0) ? (int)(rhead * p.lse_head + rpos) * 4 : kOOB;
+            li[rt] = (rok ? lim_r(rpos) : sk) - 4 * g;
+        }
+        // K row reads: key 16 kt + l16, chunk 4 s + g; V^T reads: lane 4 q + p of group g, key
+        // 4 g + q (+ 32 ks + 16 h), d 16 dt + 4 p, base per dt parity e (kv_off image)
+        const int kb0 = sbase + 2048 * ((lane >> 3) & 1) + 64 * (lane & 7) + 16 * (g ^ ((lane >> 2) & 3));
+        const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+        int vb16[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            vb16[e] = sbase + kFwdppVReg + 2048 * (g >> 1) + 64 * (4 * (g & 1) + q4) +
+                      16 * ((2 * e + (p4 >> 1)) ^ g) + 8 * (p4 & 1);
+#ifdef XFA_FWDPP16_STAMPS
+#define XFA_PP16_ACC_ARG , acc
+#else
+#define XFA_PP16_ACC_ARG
+#endif
+        if constexpr (BF16)
+            fwdpp16_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                              p.scale_log2, thr, kb0, vb16[0], vb16[1], dma0, dma0 + 128, li[0], li[1], qo[0], qo[1],
+                              oo[0], oo[1], lo[0], lo[1] XFA_PP16_ACC_ARG);
+        else
+            fwdpp16_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                             p.scale_log2, thr, kb0, vb16[0], vb16[1], dma0, dma0 + 128, li[0], li[1], qo[0], qo[1],
+                             oo[0], oo[1], lo[0], lo[1] XFA_PP16_ACC_ARG);
+#undef XFA_PP16_ACC_ARG
+        return;
+    }
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff XFA_PP_ACC_ARG);
@@ -171,7 +218,7 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
 // (n-1-i, i) row-block pairs (dense) or per-XCD dynamic queues (varlen).
-template <bool BF16>
+template <bool BF16, bool M16 = false>
 __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_claim[2];
@@ -216,7 +263,7 @@ __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
-        fwdpp_item<BF16>(p, smem, bh, m_block XFA_PP_ACC_ARG);
+        fwdpp_item<BF16, M16>(p, smem, bh, m_block XFA_PP_ACC_ARG);
     }
 #ifdef XFA_FWDPP_STAMPS
     if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwdpp_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], acc);

@@ -8,13 +8,23 @@
 
 #include <atomic>
 
+#ifndef XFA_VARIANTS
+// 0: the product library.  1 (build.py --variants, lib/variants/): also the kernels no default
+// path runs, kept for A/B and the bit-identity tests: the 4-wave D = 128 forward (fwd_w4 = 1) and
+// the 8-wave ping-pong fp8 forward (fp8_w4 = 2)
+#define XFA_VARIANTS 0
+#endif
+
 namespace xfa {
 
 // Tuning knobs, settable through fmha_set_option() (schedule choices with equal results; the
 // parity suite runs under any of them via XFA_TEST_OPTIONS).  Atomic: a launch on another
 // thread reads each knob once, as a whole value.
 struct Options {
-    std::atomic<int> fwd_w4{2};          // D = 128 forward where eligible: 2 the 8-wave ping-pong
+    std::atomic<int> fwd_w4{4};          // D = 128 forward where eligible: 4 auto (3 where no row
+                                         // has a right window, else 2); 3 the ping-pong on the
+                                         // 16x16x32 MFMA (r6: non-causal C2 +1.5-2.8 %, causal
+                                         // -1.3-3.4 % against 2, same box); 2 the 8-wave ping-pong
                                          // kernel (fmha_fwdpp_kernel.h; round 5, same box: C2 causal
                                          // +2-3 %, C4 +3 %, non-causal equal), 1 the 4-wave kernel
                                          // (fmha_fwd4_kernel.h), 0 neither (8-wave fmha_fwd_kernel)
@@ -94,6 +104,27 @@ struct AppendParams {
     int64_t page_stride, row_stride, head_stride;   // cache strides (elements)
 };
 hipError_t launch_append(const AppendParams& p, bool fp16, hipStream_t st);
+
+// Causal ALiBi LSE convention (fmha_append.hip): the kernels bias a causal score by
+// -slope |pos + diag - key| (its largest value 0 sits on the diagonal, which the in-loop
+// reference max needs), the reference by +slope key (mask_hip.h:163-164); the two differ by the
+// row constant slope (pos + diag), diag = sk - sq per sequence.  dst[row] = src[row] +
+// sign * slope (pos + diag) for finite entries: sign +1 turns the kernels' LSE into the
+// reference's (forward), -1 back (backward input).
+struct LseAlibiParams {
+    const float* src;
+    float* dst;
+    float sign;
+    const float* alibi;
+    int alibi_bstride;
+    int b, h, seqlen_q, seqlen_k;
+    const int* cu_seqlens_q;
+    const int* cu_seqlens_k;
+    const int* seqused_k;
+    const int* leftpad_k;
+    int64_t lse_batch, lse_head;
+};
+hipError_t launch_lse_alibi(const LseAlibiParams& p, hipStream_t st);
 
 // D = 256 (bucket of 129..256): 4 waves x 32 rows, one wave per SIMD (512 registers:
 // Q fragments and the O accumulator alone are 192), no LDS-DMA pipeline
