@@ -300,3 +300,64 @@ def test_fwdpp_varlen_seqused_k(xfa, causal):
         pt, _ = orc.attention_ref(qs, ks, vs, causal=causal, upcast=False, reorder_ops=True)
         ok, err, bound = orc.parity_ok(out[a_:b_][None].float(), ref, pt, 2.0, 1e-5)
         assert ok, f"seqused_k seq {i}: {err:.3g} > {bound:.3g}"
+
+
+FEAT_CASES = [
+    # b, h, hk, sq, sk, causal, window, alibi, softcap
+    (2, 4, 4, 700, 700, True, (-1, -1), True, 0.0),
+    (1, 8, 2, 513, 1025, False, (-1, -1), True, 0.0),
+    (2, 4, 4, 300, 900, True, (-1, -1), False, 30.0),
+    (1, 4, 2, 1024, 1024, False, (-1, 200), True, 20.0),
+    (2, 8, 8, 257, 129, True, (-1, -1), True, 15.0),     # sq > sk: rows with no key
+]
+
+
+@pytest.mark.parametrize("b,h,hk,sq,sk,causal,window,alibi,softcap", FEAT_CASES)
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_fwdpp_alibi_softcap(b, h, hk, sq, sk, causal, window, alibi, softcap, dt):
+    """ALiBi and softcap on the 32x32x16 ping-pong kernel's score-feature pass (the kernel id is
+    asserted): O against the oracle (test.py:975 rule; 3x with softcap, whose tanh the oracle
+    evaluates in fp32), the LSE against the fp32 log-sum-exp in the reference kernel's ALiBi form
+    (mask_hip.h:162-167), and O within bf16 rounding of the compiler-scheduled 8-wave kernel"""
+    from xf_flash_attention_cutlass_amd import capi
+    g = torch.Generator().manual_seed(sq * 3 + sk)
+    q = (torch.randn(b, sq, h, 128, generator=g) * 2).to(dt)
+    k = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    v = torch.randn(b, sk, hk, 128, generator=g).to(dt)
+    slopes = torch.rand(b, h, generator=g) * 0.3 if alibi else None
+    L = capi.lib()
+
+    def run(w4):
+        qd, kd, vd = (x.to(DEV).contiguous() for x in (q, k, v))
+        o = torch.empty_like(qd)
+        lse = torch.empty(b, h, sq, device=DEV, dtype=torch.float32)
+        sl = slopes.to(DEV).contiguous() if alibi else None
+        wl, wr = (-1, 0) if causal else window
+        old = L.fmha_get_option(b"fwd_w4")
+        assert L.fmha_set_option(b"fwd_w4", w4) == 0
+        try:
+            kern = _run(L, lambda: L.fmha_fwd(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), o.data_ptr(),
+                                              sl.data_ptr() if alibi else None, sq, sk, b, h, hk, 128, 0.0,
+                                              capi.stream_handle(), None, 128 ** -0.5, None, lse.data_ptr(),
+                                              wl, wr, softcap, False, dt == torch.float16, 1))
+        finally:
+            L.fmha_set_option(b"fwd_w4", old)
+        return o.cpu(), lse.cpu(), kern
+
+    o, lse, kern = run(4)
+    assert kern.startswith("fmha_fwdpp_kernel "), kern
+    o8, _, kern8 = run(0)
+    assert kern8.startswith("fmha_fwd_kernel"), kern8
+    bias_o = orc.alibi_bias(slopes, sq, sk, causal=causal) if alibi else None
+    w = (-1, 0) if causal else window
+    ref, _ = orc.attention_ref(q, k, v, attn_bias=bias_o, causal=causal, window_size=w, softcap=softcap)
+    pt, _ = orc.attention_ref(q, k, v, attn_bias=bias_o, causal=causal, window_size=w, softcap=softcap,
+                              upcast=False, reorder_ops=True)
+    ok, err, bound = orc.parity_ok(o.float(), ref, pt, 3.0 if softcap else 2.0, 1e-5)
+    assert ok, f"O: max|out-ref| = {err:.3g} > {bound:.3g}"
+    bias_l = orc.alibi_bias_kernel(slopes, sq, sk, causal=causal) if alibi else None
+    lref = orc.attention_lse_ref(q, k, attn_bias=bias_l, causal=causal, window_size=w, softcap=softcap)
+    fin = torch.isfinite(lref)
+    assert torch.equal(torch.isinf(lse), ~fin)
+    assert (lse[fin] - lref[fin]).abs().max().item() < 1e-3
+    assert (o.float() - o8.float()).abs().max().item() <= 4 * (pt.float() - ref).abs().max().item() + 1e-2

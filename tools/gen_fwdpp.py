@@ -72,6 +72,8 @@ DLEAD = 3              # V(j) loads tile j + DLEAD (needs RING > DLEAD: B's last
                        # is in global phase 2t+3, A's load of tile t+RING in 2(t+RING-DLEAD)+3)
 
 GUARDS = []            # assembler checks of the return-address signs, after the whole program
+FEATURES = True        # the score features (softcap, ALiBi) behind %[feat] bits, as an out-of-line
+                       # pass over S before each softmax (gen_fwd8pp / gen_fwdpp16 turn it off)
 
 
 def addc_ret(reg, ret, pc, back):
@@ -282,13 +284,75 @@ def redo_check(uid, tag):
     return inline, stub
 
 
-def v_phase(dt, slot, kind, uid, tag):
+def feat_call(uid, tag, block="feat"):
+    """(inline part, stub): with any %[feat] bit set, a score-feature block (feature_block) over
+    this tile's S before its max / softmax; returns through SRA"""
+    if not FEATURES:
+        return [], []
+    inline = ["s_cmp_lg_u32 %[feat], 0", f"s_cbranch_scc1 .Lft{tag}_{uid}", f".Lfr{tag}_{uid}:"]
+    stub = [f".Lft{tag}_{uid}:", f"s_getpc_b64 s[{SRA}:{SRA + 1}]", f".Lpf{tag}_{uid}:",
+            f"s_add_u32 s{SRA}, s{SRA}, .Lfr{tag}_{uid} - .Lpf{tag}_{uid}",
+            *addc_ret(SRA + 1, f".Lfr{tag}_{uid}", f".Lpf{tag}_{uid}", True),
+            f"s_branch .L{block}_{uid}"]
+    return inline, stub
+
+
+def _softcap_ops():
+    ops = []
+    for v in range(32):
+        sr = f"v{SBASE + v}"
+        st_ = [[f"v_mul_f32 {sr}, %[scp2], {sr}"], [f"v_exp_f32 {sr}, {sr}"],
+               [f"v_add_f32 {sr}, 1.0, {sr}"], [f"v_rcp_f32 {sr}, {sr}"],
+               [f"v_fma_f32 {sr}, {sr}, -2.0, 1.0"]]
+        for k, txt in enumerate(st_):
+            ops.append((v + 2 * k, v, txt))
+    return sum((txt for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1]))), [])
+
+
+def _alibi_ops():
+    import struct
+    base = f"v{TMP + 7}"
+    out = [f"s_add_i32 s{ST}, s{SJ}, 1", f"s_lshl_b32 s{ST}, s{ST}, 6", f"v_cvt_f32_i32 {base}, s{ST}",
+           f"v_sub_f32 {base}, %[ald], {base}"]
+    ops = []
+    for v in range(32):
+        off, _ = value_info(v)
+        t = f"v{TMP + v % 7}"
+        lit = "0x%08x" % struct.unpack("<I", struct.pack("<f", float(off)))[0]
+        st_ = [[f"v_subrev_f32 {t}, {lit}, {base}"],
+               [f"v_fma_f32 v{SBASE + v}, -%[alw], |{t}|, v{SBASE + v}"]]
+        for k, txt in enumerate(st_):
+            ops.append((v + 3 * k, v, txt))
+    return out + sum((txt for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1]))), [])
+
+
+def feature_block(uid):
+    """the score features of the 8-wave kernel's transform (fmha_fwd_kernel.h transform_part),
+    in place on this lane's 32 raw scores of tile j + 1 (SJ = j):
+      bit 0 softcap: S = tanh(S pre) = 1 - 2 / (2^(2 log2e pre S) + 1)   (%[scp2] = 2 log2e pre)
+      bit 1 ALiBi:   S -= w |pos + diag - key|   (%[alw] = slope / scale_softmax of the lane's
+                     row, %[ald] = pos + diag - 4 hh; key = 64 (j + 1) + 4 hh + off)
+    5 VALU per score for the softcap, 2 for ALiBi, staggered over the scores.  Three entries,
+    each returning via SRA: .Lfeat (both, by bit), .Lfsc (softcap by bit: tile 0 before its max)
+    and .Lfal (ALiBi by bit: tile 0 after it)."""
+    out = [f".Lfeat_{uid}:", "s_bitcmp1_b32 %[feat], 0", f"s_cbranch_scc0 .Lfa_{uid}"] + _softcap_ops()
+    out += [f".Lfa_{uid}:", "s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfe_{uid}"] + _alibi_ops()
+    out += [f".Lfe_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    out += [f".Lfsc_{uid}:", "s_bitcmp1_b32 %[feat], 0", f"s_cbranch_scc0 .Lfse_{uid}"] + _softcap_ops()
+    out += [f".Lfse_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    out += [f".Lfal_{uid}:", "s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfle_{uid}"] + _alibi_ops()
+    out += [f".Lfle_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    return out
+
+
+def v_phase(dt, slot, kind, uid, tag, feat=True):
     """V phase: kind 'u' unmasked softmax, 'm' masked, 'n' none; DMA of the tile in slot.
     Returns (inline, out-of-line stubs)."""
     pieces = dma_pieces(slot)
     if kind == "n" or ("nosm" in ABL and kind == "u"):
         return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
     sm = softmax(dt, kind == "m")
+    fin, fstub = feat_call(uid, tag) if feat else ([], [])
     if DMAMIX:
         out = pieces[0] + VPH_NOPS                      # last QK^T results -> VALU
         # the other pieces spread through the softmax
@@ -298,10 +362,10 @@ def v_phase(dt, slot, kind, uid, tag):
             sm[at:at] = pc
     else:
         out = sum(pieces, []) + VPH_NOPS
-    out += sm
+    out += fin + sm
     inl, stub = redo_check(uid, tag)
     out += inl + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"]
-    return out, stub
+    return out, stub + fstub
 
 
 ST_M, ST_MW, ST_V, ST_VW, ST_PRO, ST_TAIL, ST_EPI = range(7)
@@ -365,13 +429,27 @@ def group_program(dt, grp):
     v_wait = [] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2)})"]
     bar = ["s_barrier"]
     out, tail = [], []
+    if FEATURES:
+        out += [f"s_mov_b32 s{SJ}, -1"]                    # (tile j + 1 = 0 in the pre-loop phases)
     if grp:
         out += bar                                          # B runs one phase behind A
     # M(-1) = QK(0) (waves with a visible key), V(-1) = tile-0 max + softmax(0) (masked) + DMA
     out += st(ST_PRO) + [f"s_cmp_lt_i32 %[tw], 0", f"s_cbranch_scc1 .Lni_{uid}"]
     out += m_phase(dt, RING - 1, pv=False) + st(ST_M) + m_wait + bar + st(ST_MW)
-    v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f")
-    out += first_max() + v + st(ST_V) + v_wait + bar
+    if FEATURES:
+        # tile 0: the score features before its max (the V phase then runs none of its own)
+        # ALiBi: tile 0's max is taken on the unbiased scores and lifted by the row's best bias
+        # (%[alm] = -w * the distance from pos + diag to the row's nearest visible key), so the
+        # reference max does not lag the diagonal (causal rows' scores rise along the keys)
+        v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f", feat=False)
+        f0, s0 = feat_call(uid, "f0", "fsc")
+        f1, s1 = feat_call(uid, "f1", "fal")
+        out += XDL_NOPS + f0 + first_max() + [f"v_fma_f32 v{NM}, -%[c], %[alm], v{NM}"] + f1
+        out += v + st(ST_V) + v_wait + bar
+        stub += s0 + s1
+    else:
+        v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f")
+        out += first_max() + v + st(ST_V) + v_wait + bar
     tail += stub
     out += [f"s_branch .Lloop_{uid}", f".Lni_{uid}:"]
     # (no visible key: the same barriers and DMA duty)
@@ -419,7 +497,7 @@ def group_program(dt, grp):
     out += [f"s_cmp_eq_u32 s{SST}, 0", f"s_cbranch_scc0 .Ldone_{uid}"] + epilogue(dt)
     out += [f".Ldone_{uid}:"] + ([] if "noepiwait" in ABL else ["s_waitcnt vmcnt(0)"])
     out += st(ST_TAIL) + ["s_branch .Lend_%="]
-    return out + tail + redo_block(dt, uid)
+    return out + tail + redo_block(dt, uid) + (feature_block(uid) if FEATURES else [])
 
 
 def item_program(dt):
@@ -447,14 +525,16 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const i32x4 qsrd, const i32x4 osrd, const i32x4 lsrd, const int kstep, const int kdst, "
        "const int ntl, const int tw, const int ew, const int grp, const float c, const float thr, "
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
-       "const int lim, const int qoff, const int ooff, const int loff")
+       "const int lim, const int qoff, const int ooff, const int loff, const int feat, "
+       "const float scp2, const float alw, const float ald, const float alm")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
        '[grp] "s"(grp)', '[c] "s"(c)', '[thr] "s"(thr)',
        '[kb0] "v"(kb0)', '[kb1] "v"(kb1)', '[vb0] "v"(vb0)', '[vb1] "v"(vb1)',
        '[dma0] "v"(dma0)', '[dma1] "v"(dma1)', '[lim] "v"(lim)', '[qoff] "v"(qoff)',
-       '[ooff] "v"(ooff)', '[loff] "v"(loff)']
+       '[ooff] "v"(ooff)', '[loff] "v"(loff)', '[feat] "s"(feat)', '[scp2] "s"(scp2)',
+       '[alw] "v"(alw)', '[ald] "v"(ald)', '[alm] "v"(alm)']
 
 
 def clobbers():

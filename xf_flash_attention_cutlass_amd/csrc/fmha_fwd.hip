@@ -135,12 +135,14 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 }
 
 #if XFA_HD == 128
-// 4-wave forward (fmha_fwd4_kernel.h): dense / varlen, D = 128, one split, no left
-// window, no ALiBi / softcap / paged / fp8 K/V / leftpad (those run the 8-wave kernel)
+// 4-wave / ping-pong forwards: dense / varlen, D = 128, one split, no left window, no paged /
+// fp8 K/V / leftpad / dropout (those run the 8-wave kernel)
+// (ALiBi and softcap: the 32x32x16 ping-pong kernel only, its score-feature pass)
 static bool fwd4_eligible(const FwdParams& p) {
+    const bool feat = p.alibi || p.softcap_pre > 0.f;
     return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 &&
-           (p.wl < 0 || p.wl >= p.seqlen_k) && !p.alibi &&
-           !(p.softcap_pre > 0.f) && !p.block_table && !p.kv_fp8 && !p.leftpad_k && !p.drop;
+           (p.wl < 0 || p.wl >= p.seqlen_k) && !p.block_table && !p.kv_fp8 && !p.leftpad_k &&
+           !p.drop && (!feat || p.fwd4 == 2 || p.fwd4 == 4);
 }
 
 // 8-wave ping-pong forward (fmha_fwdpp_kernel.h): the same items, schedules and eligibility
@@ -161,7 +163,7 @@ static hipError_t launch_fwdpp(const FwdParams& p, hipStream_t st) {
     // fwd_w4 = 3: the body on the 16x16x32 MFMA shape (tools/gen_fwdpp16.py); 4 (auto, the
     // default): 16x16x32 where no row has a right window (causal / local rows: 32x32x16), the
     // faster of the two per mask on the same box
-    const bool m16 = p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0);
+    const bool m16 = p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0 && !p.alibi && !(p.softcap_pre > 0.f));
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] {
         (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);

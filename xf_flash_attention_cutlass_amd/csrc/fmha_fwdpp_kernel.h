@@ -208,12 +208,25 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
 #undef XFA_PP16_ACC_ARG
         return;
     }
+    // score features (gen_fwdpp.feature_block): bit 0 softcap, bit 1 ALiBi (the lane's row slope
+    // in raw-score units and its distance pos + diag - 4 hh to the lane's key offset 0)
+    const int feat = __builtin_amdgcn_readfirstlane((p.softcap_pre > 0.f ? 1 : 0) | (p.alibi ? 2 : 0));
+    const float scp2 = p.softcap_pre * (2.f * kLog2e);
+    const float alw = (p.alibi && ok) ? p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul : 0.f;
+    const float ald = (float)(pos + diag - 4 * hh);
+    // the row's best ALiBi bias: -w times the distance from pos + diag to its nearest visible key
+    // (keys [0, lim_r)); tile 0's reference max is lifted by it
+    const int hi_k = ok ? lim_r(pos) : 0;
+    const int near = min(max(pos + diag, 0), max(hi_k - 1, 0));
+    const float alm = hi_k > 0 ? -alw * (float)abs(pos + diag - near) : 0.f;
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff XFA_PP_ACC_ARG);
+                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
+                        feat, scp2, alw, ald, alm XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
-                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff XFA_PP_ACC_ARG);
+                       p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
+                       feat, scp2, alw, ald, alm XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
