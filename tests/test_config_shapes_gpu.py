@@ -48,7 +48,7 @@ def _rand(shape, seed, dtype=torch.bfloat16):
     return torch.randn(*shape, device=DEV, dtype=dtype, generator=g)
 
 
-SAMPLE_BH = [(0, 0), (1, 17), (3, 31)]
+SAMPLE_BH = [(0, 0), (1, 17), (2, 9), (3, 31)]     # every batch of B = 4
 
 
 def test_c2_full_shape(xfa, parity_report):

@@ -309,14 +309,21 @@ FEAT_CASES = [
     (2, 4, 4, 300, 900, True, (-1, -1), False, 30.0),
     (1, 4, 2, 1024, 1024, False, (-1, 200), True, 20.0),
     (2, 8, 8, 257, 129, True, (-1, -1), True, 15.0),     # sq > sk: rows with no key
+    # left windows (sliding / local), alone and with the features
+    (2, 4, 4, 1100, 1100, False, (255, 0), False, 0.0),
+    (1, 8, 2, 700, 1300, False, (100, 30), False, 0.0),
+    (2, 4, 2, 1300, 700, False, (64, 0), True, 0.0),      # sq > sk
+    (1, 4, 4, 2048, 2048, False, (1023, 0), True, 25.0),
+    (2, 4, 4, 777, 777, False, (0, 0), False, 0.0),       # the diagonal only
+    (1, 4, 4, 513, 513, False, (300, -1), True, 0.0),     # left window only (right = sk)
 ]
 
 
 @pytest.mark.parametrize("b,h,hk,sq,sk,causal,window,alibi,softcap", FEAT_CASES)
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_fwdpp_alibi_softcap(b, h, hk, sq, sk, causal, window, alibi, softcap, dt):
-    """ALiBi and softcap on the 32x32x16 ping-pong kernel's score-feature pass (the kernel id is
-    asserted): O against the oracle (test.py:975 rule; 3x with softcap, whose tanh the oracle
+    """ALiBi, softcap and left windows on the 32x32x16 ping-pong kernel's score-feature pass and
+    two-sided key window (the kernel id is asserted): O against the oracle (test.py:975 rule; 3x with softcap, whose tanh the oracle
     evaluates in fp32), the LSE against the fp32 log-sum-exp in the reference kernel's ALiBi form
     (mask_hip.h:162-167), and O within bf16 rounding of the compiler-scheduled 8-wave kernel"""
     from xf_flash_attention_cutlass_amd import capi
@@ -349,7 +356,7 @@ def test_fwdpp_alibi_softcap(b, h, hk, sq, sk, causal, window, alibi, softcap, d
     o8, _, kern8 = run(0)
     assert kern8.startswith("fmha_fwd_kernel"), kern8
     bias_o = orc.alibi_bias(slopes, sq, sk, causal=causal) if alibi else None
-    w = (-1, 0) if causal else window
+    w = (-1, 0) if causal else (window[0], sk) if window[0] >= 0 and window[1] < 0 else window
     ref, _ = orc.attention_ref(q, k, v, attn_bias=bias_o, causal=causal, window_size=w, softcap=softcap)
     pt, _ = orc.attention_ref(q, k, v, attn_bias=bias_o, causal=causal, window_size=w, softcap=softcap,
                               upcast=False, reorder_ops=True)

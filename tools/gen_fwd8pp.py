@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_fwdpp as pp  # noqa: E402
 
 pp.FEATURES = False    # (no softcap / ALiBi pass in this body)
+pp.LEFTWIN = False     # (no left windows: the one-sided key limit)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "xf_flash_attention_cutlass_amd", "csrc", "fmha_fwd8pp_body.h")

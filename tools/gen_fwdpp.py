@@ -74,6 +74,9 @@ DLEAD = 3              # V(j) loads tile j + DLEAD (needs RING > DLEAD: B's last
 GUARDS = []            # assembler checks of the return-address signs, after the whole program
 FEATURES = True        # the score features (softcap, ALiBi) behind %[feat] bits, as an out-of-line
                        # pass over S before each softmax (gen_fwd8pp / gen_fwdpp16 turn it off)
+LEFTWIN = True         # two-sided key window in the masked steps (left windows: keys
+                       # [LIML, LIML + %[wid]) of the tile, relative to this lane's offset 0)
+LIML, TW = 96, 97      # the lane's left key limit (stepped -64 per tile); a compare temp
 
 
 def addc_ret(reg, ret, pc, back):
@@ -206,6 +209,17 @@ def dma_advance():
     return out
 
 
+def vis_test(off):
+    """vcc = key offset `off` (of this lane's keys in the tile) is visible to its row"""
+    if LEFTWIN:   # (unsigned) off - LIML < wid <=> LIML <= off < LIML + wid = the right limit
+        return [f"v_sub_u32 v{TW}, {off}, v{LIML}", f"v_cmp_lt_u32 vcc, v{TW}, %[wid]"]
+    return [f"v_cmp_lt_i32 vcc, {off}, v{LIM}"]
+
+
+def lim_step():
+    return [f"v_add_u32 v{LIM}, -64, v{LIM}"] + ([f"v_add_u32 v{LIML}, -64, v{LIML}"] if LEFTWIN else [])
+
+
 def softmax(dt, mask):
     """P = exp2(S c - m) of this lane's 32 scores (masked: keys at or past the lane's limit give
     0), the tile row sum in LT; 4 scores in flight"""
@@ -215,7 +229,7 @@ def softmax(dt, mask):
         off, dword = value_info(v)
         ex = [f"v_exp_f32 {t}, {t}"]
         if mask:
-            ex += [f"v_cmp_lt_i32 vcc, {off}, v{LIM}", f"v_cndmask_b32 {t}, 0, {t}, vcc"]
+            ex += vis_test(off) + [f"v_cndmask_b32 {t}, 0, {t}, vcc"]
         st = [[f"v_fma_f32 {t}, v{SBASE + v}, %[c], v{NM}"], ex,
               [f"v_mov_b32 v{LT}, {t}" if v == 0 else f"v_add_f32 v{LT}, v{LT}, {t}"]]
         if v & 1:
@@ -228,22 +242,41 @@ def softmax(dt, mask):
     return out + ["s_nop 0"]
 
 
-def row_max(dst):
-    """masked max of this lane's row over the tile's 64 keys (both lane halves) -> dst"""
+def row_max(dst, raw=None):
+    """masked max of this lane's row over the tile's 64 keys (both lane halves) -> dst (and the
+    unmasked max -> raw)"""
     t2, ninf = f"v{MISC + 1}", f"v{MISC + 3}"
     out = [f"v_mov_b32 {ninf}, 0xff800000", f"v_mov_b32 {dst}, {ninf}"]
+    if raw:
+        out.append(f"v_mov_b32 {raw}, {ninf}")
     for v in range(32):
         off, _ = value_info(v)
-        out += [f"v_cmp_lt_i32 vcc, {off}, v{LIM}",
-                f"v_cndmask_b32 {t2}, {ninf}, v{SBASE + v}, vcc",
-                f"v_max_f32 {dst}, {dst}, {t2}"]
-    return out + [f"v_mov_b32 {t2}, {dst}", "s_nop 1", f"v_permlane32_swap_b32 {dst}, {t2}",
-                  "s_nop 1", f"v_max_f32 {dst}, {dst}, {t2}"]
+        out += vis_test(off) + [f"v_cndmask_b32 {t2}, {ninf}, v{SBASE + v}, vcc",
+                                f"v_max_f32 {dst}, {dst}, {t2}"]
+        if raw:
+            out.append(f"v_max_f32 {raw}, {raw}, v{SBASE + v}")
+    out += [f"v_mov_b32 {t2}, {dst}", "s_nop 1", f"v_permlane32_swap_b32 {dst}, {t2}",
+            "s_nop 1", f"v_max_f32 {dst}, {dst}, {t2}"]
+    if raw:
+        out += [f"v_mov_b32 {t2}, {raw}", "s_nop 1", f"v_permlane32_swap_b32 {raw}, {t2}",
+                "s_nop 1", f"v_max_f32 {raw}, {raw}, {t2}"]
+    return out
 
 
 def first_max():
-    """m = the masked max of tile 0 (in log2 units: NM = -c max, 0 for a row with no key)"""
+    """m = the masked max of tile 0 (in log2 units: NM = -c max; 0 for a row with no key).
+    LEFTWIN: a row with no visible key in tile 0 (its window starts later) takes NM = +inf, so
+    its first visible key gives P = inf and the redo path sets m to that tile's true max — the
+    row's reference max is then exact, as tile 0's is for the others (a single-key row gets
+    P = 1 and O = its V row bit for bit)"""
     mx, t2 = f"v{MISC}", f"v{MISC + 1}"
+    if LEFTWIN:
+        pinf = f"v{MISC + 3}"
+        return XDL_NOPS + row_max(mx) + [
+            f"v_mul_f32_e64 {t2}, -%[c], {mx}",
+            f"v_cmp_lg_f32 vcc, 0xff800000, {mx}",
+            f"v_mov_b32 {pinf}, 0x7f800000",           # (a literal and vcc: two constant-bus reads)
+            f"v_cndmask_b32 v{NM}, {pinf}, {t2}, vcc"]
     return XDL_NOPS + row_max(mx) + [
         f"v_mul_f32_e64 {t2}, -%[c], {mx}",
         f"v_cmp_lg_f32 vcc, 0xff800000, {mx}",
@@ -258,6 +291,9 @@ def redo_block(dt, uid):
     out = [f".Lredo_{uid}:"] + XDL_NOPS + row_max(mx)
     out += [f"v_mul_f32 {t2}, %[c], {mx}",
             f"v_max_f32_e64 {t2}, {t2}, -v{NM}",          # m_new = max(m_ref, c max)
+            # (LEFTWIN: a row still at NM = +inf with no visible key here keeps m_new finite,
+            # -FLT_MAX, so alpha = 2^(m - m_new) = 0, not NaN; its O and l are 0)
+            *([f"v_max_f32 {t2}, 0xff7fffff, {t2}"] if LEFTWIN else []),
             f"v_add_f32 {alpha}, v{NM}, {t2}",             # m_new - m_ref >= 0
             f"v_exp_f32_e64 {alpha}, -{alpha}",
             f"v_mul_f32 v{NM}, -1.0, {t2}",
@@ -350,7 +386,7 @@ def v_phase(dt, slot, kind, uid, tag, feat=True):
     Returns (inline, out-of-line stubs)."""
     pieces = dma_pieces(slot)
     if kind == "n" or ("nosm" in ABL and kind == "u"):
-        return sum(pieces, []) + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"], []
+        return sum(pieces, []) + dma_advance() + lim_step(), []
     sm = softmax(dt, kind == "m")
     fin, fstub = feat_call(uid, tag) if feat else ([], [])
     if DMAMIX:
@@ -364,7 +400,7 @@ def v_phase(dt, slot, kind, uid, tag, feat=True):
         out = sum(pieces, []) + VPH_NOPS
     out += fin + sm
     inl, stub = redo_check(uid, tag)
-    out += inl + dma_advance() + [f"v_add_u32 v{LIM}, -64, v{LIM}"]
+    out += inl + dma_advance() + lim_step()
     return out, stub + fstub
 
 
@@ -464,6 +500,8 @@ def group_program(dt, grp):
         out += st(ST_VW) + [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
+        if LEFTWIN:   # tiles before lw cross some row's left window edge
+            out += [f"s_cmp_ge_i32 s{ST}, %[lw]", f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         # unmasked step (inline)
         out += m_phase(dt, ph) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, stub = v_phase(dt, vslot, "u", uid, f"u{ph}")
@@ -504,6 +542,7 @@ def item_program(dt):
     out = (["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_mov_b32 s98, s96"] if STAMPS else [])
     out += ["s_waitcnt lgkmcnt(0)",
            f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LIM}, %[lim]",
+           *([f"v_mov_b32 v{LIML}, %[liml]"] if LEFTWIN else []),
            f"s_mov_b32 s{SST}, 0"]
     if not ABL & {"nopro", "nopq"}:
         out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
@@ -526,7 +565,8 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const int ntl, const int tw, const int ew, const int grp, const float c, const float thr, "
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
        "const int lim, const int qoff, const int ooff, const int loff, const int feat, "
-       "const float scp2, const float alw, const float ald, const float alm")
+       "const float scp2, const float alw, const float ald, const float alm, const int lw, "
+       "const int liml, const int wid")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
@@ -534,11 +574,12 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[kb0] "v"(kb0)', '[kb1] "v"(kb1)', '[vb0] "v"(vb0)', '[vb1] "v"(vb1)',
        '[dma0] "v"(dma0)', '[dma1] "v"(dma1)', '[lim] "v"(lim)', '[qoff] "v"(qoff)',
        '[ooff] "v"(ooff)', '[loff] "v"(loff)', '[feat] "s"(feat)', '[scp2] "s"(scp2)',
-       '[alw] "v"(alw)', '[ald] "v"(ald)', '[alm] "v"(alm)']
+       '[alw] "v"(alw)', '[ald] "v"(ald)', '[alm] "v"(alm)', '[lw] "s"(lw)', '[liml] "v"(liml)',
+       '[wid] "v"(wid)']
 
 
 def clobbers():
-    regs = [f'"v{i}"' for i in range(96)] + [f'"a{i}"' for i in range(128)]
+    regs = [f'"v{i}"' for i in range(98 if LEFTWIN else 96)] + [f'"a{i}"' for i in range(128)]
     regs += [f'"s{i}"' for i in range(SKR, SCM + 2)] + ([f'"s{i}"' for i in range(96, 100)] if STAMPS else [])
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 

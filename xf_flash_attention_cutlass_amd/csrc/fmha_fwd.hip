@@ -135,14 +135,14 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 }
 
 #if XFA_HD == 128
-// 4-wave / ping-pong forwards: dense / varlen, D = 128, one split, no left window, no paged /
-// fp8 K/V / leftpad / dropout (those run the 8-wave kernel)
-// (ALiBi and softcap: the 32x32x16 ping-pong kernel only, its score-feature pass)
+// 4-wave / ping-pong forwards: dense / varlen, D = 128, one split, no paged / fp8 K/V /
+// leftpad / dropout (those run the 8-wave kernel)
+// (ALiBi, softcap and left windows: the 32x32x16 ping-pong kernel only, its score-feature pass
+// and two-sided key window)
 static bool fwd4_eligible(const FwdParams& p) {
-    const bool feat = p.alibi || p.softcap_pre > 0.f;
-    return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 &&
-           (p.wl < 0 || p.wl >= p.seqlen_k) && !p.block_table && !p.kv_fp8 && !p.leftpad_k &&
-           !p.drop && (!feat || p.fwd4 == 2 || p.fwd4 == 4);
+    const bool feat = p.alibi || p.softcap_pre > 0.f || (p.wl >= 0 && p.wl < p.seqlen_k);
+    return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 && !p.block_table &&
+           !p.kv_fp8 && !p.leftpad_k && !p.drop && (!feat || p.fwd4 == 2 || p.fwd4 == 4);
 }
 
 // 8-wave ping-pong forward (fmha_fwdpp_kernel.h): the same items, schedules and eligibility

@@ -83,22 +83,32 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int diag = sk - sq;
     auto lim_r = [&](int pos) { return p.wr >= 0 ? min(sk, pos + diag + p.wr + 1) : sk; };
 
-    // key tiles of the workgroup: [0, ntl)
+    // left window (wl >= 0, the 32x32 body only): keys [lim_l(pos), lim_r(pos))
+    auto lim_l = [&](int pos) { return p.wl >= 0 ? max(0, pos + diag - p.wl) : 0; };
+
+    // key tiles of the workgroup: [T0, T0 + ntl) — T0 > 0 when the item's first row's window
+    // starts past key 0; the body counts tiles from T0 (K / V bases, limits shifted by 64 T0)
     const int pos_hi = (min(row0 + kFwdppRows, rows_total) - 1) / G;
     const int n_hi = sk > 0 ? lim_r(pos_hi) : 0;
-    const int ntl = n_hi > 0 ? (n_hi + kBlockN - 1) / kBlockN : 0;
+    const int ntl_abs = n_hi > 0 ? (n_hi + kBlockN - 1) / kBlockN : 0;
+    const int T0 = (M16 || ntl_abs <= 0) ? 0 : min(lim_l(row0 / G) / kBlockN, ntl_abs - 1);
+    const int ntl = ntl_abs - T0;
 
-    // this wave: rows wrow0 .. wrow0 + 31; last tile t_w; tiles >= e_w need the edge mask
+    // this wave: rows wrow0 .. wrow0 + 31; last tile t_w; tiles >= e_w need the right edge mask,
+    // tiles < l_w the left one
     const int wrow0 = row0 + 32 * wave;
-    int t_w = -1, e_w = 1 << 30;
+    int t_w = -1, e_w = 1 << 30, l_w = 0;
     if (wrow0 < rows_total && ntl > 0) {
         const int wp_lo = wrow0 / G, wp_hi = (min(wrow0 + 32, rows_total) - 1) / G;
         const int lr_hi = lim_r(wp_hi), lr_lo = lim_r(wp_lo);
-        t_w = lr_hi > 0 ? min(ntl, (lr_hi + kBlockN - 1) / kBlockN) - 1 : -1;
-        e_w = lr_lo > 0 ? lr_lo / kBlockN : 0;
+        t_w = lr_hi > 0 ? min(ntl_abs, (lr_hi + kBlockN - 1) / kBlockN) - 1 - T0 : -1;
+        t_w = max(t_w, -1);
+        e_w = (lr_lo > 0 ? lr_lo / kBlockN : 0) - T0;
+        l_w = (lim_l(wp_hi) + kBlockN - 1) / kBlockN - T0;
     }
     t_w = __builtin_amdgcn_readfirstlane(t_w);
     e_w = __builtin_amdgcn_readfirstlane(e_w);
+    l_w = __builtin_amdgcn_readfirstlane(l_w);
 
     // this lane's row
     const int row = wrow0 + lr;
@@ -108,8 +118,11 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int qoff = ok ? (pos * (int)p.q_row + head * (int)p.q_head) * 2 + 16 * hh : kOOB;
     const int ooff = ok ? (pos * (int)p.o_row + head * (int)p.o_head) * 2 + 16 * hh : kOOB;
     const int loff = (ok && hh == 0) ? (int)(head * p.lse_head + pos) * 4 : kOOB;
-    // key limit of tile 0 for this lane's keys (offset 4*hh folded in); other rows: none
-    const int lim = (ok ? lim_r(pos) : sk) - 4 * hh;
+    // key limits of tile 0 (absolute tile T0) for this lane's keys (offset 4*hh folded in);
+    // other rows: none
+    const int lim = (ok ? lim_r(pos) : sk) - 4 * hh - kBlockN * T0;
+    const int liml = (ok ? lim_l(pos) : 0) - 4 * hh - kBlockN * T0;
+    const int wid = max(lim - liml, 0);
 
     if (ntl <= 0) {
         // no visible key for any row: O = 0, LSE = +inf (the reference's empty-row output)
@@ -134,11 +147,12 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int64_t lbytes = p.lse ? ((int64_t)(p.h - 1) * p.lse_head + sq) * 4 : 0;
     const i32x4 lsrd = fwdpp_srd(lseq, (uint32_t)min(lbytes, (int64_t)kOOB - 1));
     const int k_row = (int)p.k_row;
+    const int64_t k0 = (int64_t)k_off + (int64_t)kBlockN * T0;   // the item's first key row
     const char* kseq = reinterpret_cast<const char*>(p.k) +
-                       ((int64_t)bidx * p.k_batch + (int64_t)k_off * p.k_row + (int64_t)hk_i * p.k_head) * 2;
+                       ((int64_t)bidx * p.k_batch + k0 * p.k_row + (int64_t)hk_i * p.k_head) * 2;
     const char* vseq = reinterpret_cast<const char*>(p.v) +
-                       ((int64_t)bidx * p.v_batch + (int64_t)k_off * p.v_row + (int64_t)hk_i * p.v_head) * 2;
-    const int nk = min(sk, ntl * kBlockN);
+                       ((int64_t)bidx * p.v_batch + k0 * p.v_row + (int64_t)hk_i * p.v_head) * 2;
+    const int nk = min(sk, ntl_abs * kBlockN) - kBlockN * T0;
     const int kvbytes = __builtin_amdgcn_readfirstlane((int)(((nk - 1) * k_row + HD) * 2));
     const int kblo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)kseq);
     const int kbhi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)kseq >> 32) & 0xFFFF);
@@ -213,20 +227,20 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int feat = __builtin_amdgcn_readfirstlane((p.softcap_pre > 0.f ? 1 : 0) | (p.alibi ? 2 : 0));
     const float scp2 = p.softcap_pre * (2.f * kLog2e);
     const float alw = (p.alibi && ok) ? p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul : 0.f;
-    const float ald = (float)(pos + diag - 4 * hh);
+    const float ald = (float)(pos + diag - 4 * hh - kBlockN * T0);
     // the row's best ALiBi bias: -w times the distance from pos + diag to its nearest visible key
-    // (keys [0, lim_r)); tile 0's reference max is lifted by it
-    const int hi_k = ok ? lim_r(pos) : 0;
-    const int near = min(max(pos + diag, 0), max(hi_k - 1, 0));
-    const float alm = hi_k > 0 ? -alw * (float)abs(pos + diag - near) : 0.f;
+    // (keys [lim_l, lim_r)); tile 0's reference max is lifted by it
+    const int hi_k = ok ? lim_r(pos) : 0, lo_k = ok ? lim_l(pos) : 0;
+    const int near = min(max(pos + diag, lo_k), max(hi_k - 1, lo_k));
+    const float alm = hi_k > lo_k ? -alw * (float)abs(pos + diag - near) : 0.f;
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        feat, scp2, alw, ald, alm XFA_PP_ACC_ARG);
+                        feat, scp2, alw, ald, alm, l_w, liml, wid XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                       feat, scp2, alw, ald, alm XFA_PP_ACC_ARG);
+                       feat, scp2, alw, ald, alm, l_w, liml, wid XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
