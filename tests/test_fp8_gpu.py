@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from oracle import attention_ref as orc
+from tests.fp8_model import attention_fp8_kernel_model
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -48,14 +49,26 @@ def _check(xfa, b, h, hk, sq, sk, causal=False, window=(-1, -1), seed=0, out_dty
     pt = orc.attention_fp8_pt(q8, k8, v8, qs, ks, vs, causal=causal, window_size=w).to(out_dtype)
     ok, err, bound = orc.parity_ok(out.cpu().float(), ref, pt, 3.0, 1e-3)
     if report:
-        report({"case": f"fp8 fwd b{b} h{h}/{hk} {sq}x{sk} c{causal} w{window}", "err": err,
-                "bound": bound, "ok": bool(ok)})
+        row = {"case": f"fp8 fwd b{b} h{h}/{hk} {sq}x{sk} c{causal} w{window}", "err": err,
+               "bound": bound, "ok": bool(ok)}
+        if _w4_ran():
+            # the error of the kernel's own arithmetic (tests/fp8_model.py: P against the tile-0
+            # reference max, not the row max): the cause of the cases close to their bound
+            mdl = attention_fp8_kernel_model(q8, k8, v8, qs, ks, vs, causal=causal,
+                                             window_size=w).to(out_dtype)
+            row["model_err"] = (mdl.float() - ref).abs().max().item()
+        report(row)
     assert ok, f"max|out-ref|={err:.3g} > {bound:.3g}"
     lref = orc.attention_lse_ref(qd, kd, causal=causal, window_size=w)
     fin = torch.isfinite(lref)
     assert torch.equal(torch.isinf(lse.cpu()), ~fin)
     assert (lse.cpu()[fin] - lref[fin]).abs().max().item() < 1e-3
     return out
+
+
+def _w4_ran():
+    from xf_flash_attention_cutlass_amd import capi
+    return capi.lib().fmha_last_kernel().decode().startswith("fmha_fwd8w_kernel")
 
 
 def _assert_fp8_w4():

@@ -718,7 +718,7 @@ def test_fwd_varlen_dynamic_queue_bitexact(xfa, causal):
 
 # ------------------------------------------------------------------- head dims 129..256 ---
 # The reference dispatches head-dim buckets up to 256 (static_switch.h:90-117); D in
-# (128, 256] runs the 4-wave, 512-register build of the forward kernel (DESIGN.md §3.1).
+# (128, 256] runs the 4-wave, 512-register build of the forward kernel (DESIGN.md §3.2).
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("d", [136, 160, 192, 256])

@@ -41,7 +41,7 @@ Register map (per lane):
 Even steps: S_{j+2} -> A, scores of j+1 in B, P_j in A, P_{j+1} -> B (odd steps swap).
 
 The LDS image, fragment maps and P pair order are those of the 8-wave kernel
-(fmha_fwd_kernel.h, DESIGN.md 3.1).
+(fmha_fwd_kernel.h, DESIGN.md §3.2).
 
   python tools/gen_fwd4.py   (writes xf_flash_attention_cutlass_amd/csrc/fmha_fwd4_body.h)
 """

@@ -65,12 +65,28 @@ NDMA = 4              # LDS-DMA wave-instructions per step (2 K + 2 V pieces)
 LEAD2 = True          # DMA one more step ahead: step j issues K_{j+5}, V_{j+3} (the 4-slot rings
                       # allow it) and the mid-point wait keeps two steps' pieces in flight
 ABL = set()           # timing ablations of the main-loop steps (results INVALID): nodma nosm nobar nolgkm
+STAMPS = False        # diagnostic phase stamps (--stamps, XFA_FWD8_STAMPS; tools/fwd8_stamps.py)
 
 QK, SM, PV = 1, 2, 4
 MNEM = "v_mfma_scale_f32_32x32x64_f8f6f4"
 
 
 GUARDS = []   # assembler checks of the return-address signs, emitted after the whole program
+
+# phase classes of the stamps build: the cycles since the previous stamp go to the class named
+ST_U, ST_W, ST_M, ST_I, ST_REDO, ST_PRO, ST_EPI, ST_TAIL = range(8)
+ST_NAMES = ["unmasked run", "mid-step wait", "masked run", "idle step", "redo", "prologue",
+            "epilogue", "exit drain"]
+
+
+def st(k):
+    """stamp (STAMPS builds only): s_memtime, the delta into lane k of %[acc].  Its
+    lgkmcnt(0) also retires the LDS reads in flight, so read the build's SHARES, not its times."""
+    if not STAMPS:
+        return []
+    return ["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_sub_u32 s99, s96, s98", "s_mov_b32 s98, s96",
+            f"v_readlane_b32 s97, %[acc], {k}", "s_nop 3", "s_add_u32 s97, s97, s99", "s_nop 3",
+            f"v_writelane_b32 %[acc], s97, {k}"]
 
 
 def addc_ret(reg, ret, pc, back):
@@ -171,8 +187,10 @@ def prefetch_order():
     return [("N", f) for f in range(4)] + [("W", dt) for dt in range(NWPRE)]
 
 
-def step_body(ph, kind, mask, vm=None):
-    """instructions of one step at ring phase ph (= j mod 4)"""
+def step_body(ph, kind, mask, vm=None, stc=None):
+    """instructions of one step at ring phase ph (= j mod 4); stc = (class of the first half,
+    class of its mid-point wait) for the stamps build"""
+    run_c, wait_c = stc if stc else (ST_PRO, ST_PRO)
     par = ph & 1
     sn_buf, sc_buf = (0, 1) if par == 0 else (1, 0)      # S_{j+2} -> sn, scores of j+1 in sc
     pc_buf, pn_buf = (0, 1) if par == 0 else (1, 0)      # P_j in pc, P_{j+1} -> pn
@@ -258,7 +276,7 @@ def step_body(ph, kind, mask, vm=None):
         for w, i in dmas:
             a, b = dma(w, i)
             out += [a, "s_nop 0", b]
-        out += [f"s_waitcnt vmcnt({vm})", "s_barrier"]
+        out += st(run_c) + [f"s_waitcnt vmcnt({vm})", "s_barrier"] + st(wait_c)
         for _, _, txt in sorted(sm, key=lambda x: (x[0], x[1])):
             out += txt
         out += [r[2] for r in sorted(reads, key=lambda x: (x[0], x[1]))]
@@ -302,7 +320,8 @@ def step_body(ph, kind, mask, vm=None):
                 waited = len(issued) - n
             body.append(mfma[g])
             if g == mid:
-                body += [] if ("nobar" in ABL and main) else [f"s_waitcnt vmcnt({vm})", "s_barrier"]
+                body += [] if ("nobar" in ABL and main) else (
+                    st(run_c) + [f"s_waitcnt vmcnt({vm})", "s_barrier"] + st(wait_c))
         else:
             if not (smby.get(g) or dma_gap.get(g) or rby.get(g)):
                 continue
@@ -394,12 +413,13 @@ def redo_block(par, uid):
         out.append("s_nop 1")
         out += softmax_block(sc_buf, pn_buf, rb * 32, rb * 32 + 32)
         out.append("s_nop 1")
-    out += ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    out += ["s_nop 3"] + st(ST_REDO) + [f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
     return out
 
 
 def item_program(dt, uid="%="):
-    out = ["s_waitcnt lgkmcnt(0)"]
+    out = (["s_memtime s[96:97]", "s_waitcnt lgkmcnt(0)", "s_mov_b32 s98, s96"] if STAMPS else [])
+    out += ["s_waitcnt lgkmcnt(0)"]
     out += [f"v_mov_b32 v{PINF}, 0x7f800000", f"v_mov_b32 v{NINF}, 0xff800000",
             f"v_mov_b32 v{SC127}, 0x7f",
             f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{NM + 1}, 0",
@@ -450,8 +470,8 @@ def item_program(dt, uid="%="):
 def main_loop(uid, dt):
     """per phase the unmasked step falls through into the next phase; the masked and idle steps
     and the redo stubs live after the loop and branch back (gen_fwd4.py main_loop_ff)"""
-    out = [f"s_mov_b32 s{SJ}, 0", f"s_mov_b32 s{SKO}, 0",      # SKO: rows stored (EPI_IDLE)
-           f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
+    out = st(ST_PRO) + [f"s_mov_b32 s{SJ}, 0", f"s_mov_b32 s{SKO}, 0",      # SKO: rows stored (EPI_IDLE)
+                        f"s_cmp_ge_i32 s{SJ}, %[ntl]", f"s_cbranch_scc1 .Lexit_{uid}"]
     tail = []
     for ph in range(4):
         par = ph & 1
@@ -460,19 +480,19 @@ def main_loop(uid, dt):
         out += [f"s_cmp_gt_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Li{ph}_{uid}",
                 f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
                 f"s_cbranch_scc0 .Lm{ph}_{uid}"]
-        out += step_body(ph, QK | SM | PV, False)
-        inl, stub = redo_check_ff(par, uid, f"u{ph}")
-        out += inl
+        out += step_body(ph, QK | SM | PV, False, stc=(ST_U, ST_W))
+        inl, stub = redo_check_ff(par, uid, f"u{ph}", ST_U)
+        out += inl + st(ST_U)
         tail += stub
         out.append(f".Lnx{ph}_{uid}:")
         out += [f"s_add_i32 s{SJ}, s{SJ}, 1", f"s_cmp_ge_i32 s{SJ}, %[ntl]",
                 f"s_cbranch_scc1 .Lexit_{uid}"]
         tail.append(f".Lm{ph}_{uid}:")
-        tail += step_body(ph, QK | SM | PV, True)
-        inl, stub = redo_check_ff(par, uid, f"m{ph}")
-        tail += inl + [f"s_branch .Lnx{ph}_{uid}"] + stub
+        tail += step_body(ph, QK | SM | PV, True, stc=(ST_M, ST_W))
+        inl, stub = redo_check_ff(par, uid, f"m{ph}", ST_M)
+        tail += inl + st(ST_M) + [f"s_branch .Lnx{ph}_{uid}"] + stub
         tail.append(f".Li{ph}_{uid}:")
-        tail += step_body(ph, 0, False)
+        tail += step_body(ph, 0, False, stc=(ST_I, ST_I)) + st(ST_I)
         # first idle step (after its barrier): the rows' epilogue, once
         tail += [f"s_cmp_eq_u32 s{SKO}, 0", f"s_cbranch_scc0 .Lnx{ph}_{uid}",
                  f"s_mov_b32 s{SKO}, 1",
@@ -485,7 +505,7 @@ def main_loop(uid, dt):
     return out + tail + epilogue_idle(uid, dt)
 
 
-def redo_check_ff(par, uid, tag):
+def redo_check_ff(par, uid, tag, stc=ST_U):
     """redo_check with the common case falling through (a not-taken branch to an out-of-line
     stub that sets the return address); returns (inline part, stub)"""
     inline = [f"v_cmp_lt_f32 vcc, %[thr], v{LT}",
@@ -498,7 +518,7 @@ def redo_check_ff(par, uid, tag):
               f"v_add_f32 v{LRUN + 1}, v{LRUN + 1}, v{LT + 1}"]
     # the return point lies BEFORE the stub: a negative offset, so the high word adds its sign
     # extension (-1) with the carry
-    stub = [f".Lrc{tag}_{uid}:",
+    stub = [f".Lrc{tag}_{uid}:"] + st(stc) + [
             f"s_getpc_b64 s[{SRA}:{SRA + 1}]",
             f".Lpc{tag}_{uid}:",
             f"s_add_u32 s{SRA}, s{SRA}, .Lnr{tag}_{uid} - .Lpc{tag}_{uid}",
@@ -510,16 +530,16 @@ def redo_check_ff(par, uid, tag):
 def epilogue(dt, uid):
     """O = v_scale O / l as 16-byte rows of the output dtype (permlane32 exchange), LSE; skipped
     by a wave that stored its rows in its first idle step (gen_fwd4.py EPI_IDLE)"""
-    return ([f".Lexit_{uid}:", "s_waitcnt vmcnt(0) lgkmcnt(0)",
-             f"s_cmp_eq_u32 s{SKO}, 1", f"s_cbranch_scc1 .Lend_{uid}",
+    return ([f".Lexit_{uid}:", "s_waitcnt vmcnt(0) lgkmcnt(0)"] + st(ST_TAIL) +
+            [f"s_cmp_eq_u32 s{SKO}, 1", f"s_cbranch_scc1 .Lend_{uid}",
              "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"] + epilogue_core(dt) +
-            [f".Lend_{uid}:"])
+            [f".Lend_{uid}:"] + (["s_waitcnt vmcnt(0)"] + st(ST_EPI) if STAMPS else []))
 
 
 def epilogue_idle(uid, dt):
     """the epilogue as a routine for a wave's first idle step (return address in SRA)"""
-    return ([f".Lepi_{uid}:", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"] +
-            epilogue_core(dt) + [f"s_setpc_b64 s[{SRA}:{SRA + 1}]"])
+    return ([f".Lepi_{uid}:"] + st(ST_I) + ["s_nop 7", "s_nop 7", "s_nop 7", "s_nop 7", "s_nop 3"] +
+            epilogue_core(dt) + st(ST_EPI) + [f"s_setpc_b64 s[{SRA}:{SRA + 1}]"])
 
 
 def epilogue_core(dt):
@@ -564,7 +584,7 @@ def epilogue_core(dt):
 
 def clobbers():
     regs = [f'"v{i}"' for i in range(NVFIX)] + [f'"a{i}"' for i in range(256)]
-    regs += [f'"s{i}"' for i in range(SKR, SCM + 2)]
+    regs += [f'"s{i}"' for i in range(SKR, SCM + 2)] + ([f'"s{i}"' for i in range(96, 100)] if STAMPS else [])
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 
 
@@ -590,6 +610,7 @@ def emit(out=OUT):
         "#pragma once",
         '#include "fmha_common.h"',
         "",
+        *(["#define XFA_FWD8_STAMPS 1            // diagnostic build (--stamps)"] if STAMPS else []),
         "namespace xfa {",
         "typedef __attribute__((ext_vector_type(4))) int i32x4;",
         "",
@@ -599,11 +620,12 @@ def emit(out=OUT):
         prog = item_program(dt)
         prog += GUARDS
         GUARDS.clear()
-        lines.append(f"__device__ __forceinline__ void fwd8_item_{dt}({SIG}) {{")
+        sig = SIG + (", unsigned& acc" if STAMPS else "")
+        lines.append(f"__device__ __forceinline__ void fwd8_item_{dt}({sig}) {{")
         lines.append("    asm volatile(")
         for b in prog:
             lines.append(f'        "{b}\\n"')
-        lines.append("        :")
+        lines.append('        : [acc] "+v"(acc)' if STAMPS else "        :")
         lines.append("        : " + ",\n          ".join(ops))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
@@ -620,9 +642,11 @@ if __name__ == "__main__":
     ap.add_argument("--no-lead2", dest="lead2", action="store_false",
                     help="DMA two steps ahead only (3 V^T fragments prefetched)")
     ap.add_argument("--qklead", type=int, default=QK_LEAD, help="QK MFMAs before the first PV MFMA")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic phase stamps (XFA_FWD8_STAMPS)")
     ap.add_argument("--out", default=OUT)
     a = ap.parse_args()
     ABL = set(x for x in a.abl.split(",") if x)
+    STAMPS = a.stamps
     QK_LEAD = a.qklead
     LEAD2 = a.lead2
     # LEAD2: V_{j+3} overwrites V_{j-1}'s slot in step j's first half, before its mid barrier, so

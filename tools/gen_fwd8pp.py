@@ -1,5 +1,5 @@
 """Generate csrc/fmha_fwd8pp_body.h: the 8-wave ping-pong fp8 (e4m3fn) forward body
-(csrc/fmha_fwd8pp_kernel.h; DESIGN.md 3.5).
+(csrc/fmha_fwd8pp_kernel.h; DESIGN.md §3.5).
 
 The phase program of tools/gen_fwdpp.py (read its docstring: two waves per SIMD, waves 4-7 one
 phase behind waves 0-3, MFMA phases PV(j) + QK^T(j+1) against VALU phases softmax(j+1) +
@@ -7,7 +7,7 @@ LDS-DMA, the unmasked / masked / last / idle step variants, the rare redo path) 
 layouts of the 4-wave fp8 kernel (tools/gen_fwd8.py): both GEMMs on the block-scaled
 v_mfma_scale_f32_32x32x64_f8f6f4 (E8M0 scales 1.0, 64 cycles per MFMA), a wave of 32 query rows
 per 64-key tile runs 4 QK^T + 4 PV MFMAs (512 cycles) against its 32 scores' softmax, which is
-where the 4-wave fp8 kernel spent its time (VALU-bound, DESIGN.md 3.5): here the partner wave's
+where the 4-wave fp8 kernel spent its time (VALU-bound, DESIGN.md §3.5): here the partner wave's
 MFMAs run beside it.
 
 This module imports gen_fwdpp and rebinds its operand-specific pieces (fragment reads, MFMAs,

@@ -1,5 +1,5 @@
 """Generate csrc/fmha_fwdpp_body.h: the hand-scheduled body of the 8-wave "ping-pong" D = 128
-forward (csrc/fmha_fwdpp_kernel.h; DESIGN.md 3.1c).
+forward (csrc/fmha_fwdpp_kernel.h; DESIGN.md §3.1).
 
 Round 5's structure (probe: tools/gen_pingpong.py): one workgroup = 8 waves x
 32 query rows = the 4-wave kernel's 256-row item, TWO waves per SIMD (waves w and w + 4), each
@@ -15,7 +15,7 @@ issues MFMAs while its partner issues VALU / DMA.  K / V tiles live in 4-slot LD
 kv_off image of the 4-wave kernel); tile t is published at the barrier that closes global phase
 2t-1 (group A: s_waitcnt vmcnt(4) after its V phase, group B: vmcnt(0) after its M phase).
 Measured (probe, C2 shape non-causal, two boxes): 12-13 % more work per clock than the 4-wave
-kernel, 3-4 % more per second at the 1.4 kW board power cap (DESIGN.md 3.1c).
+kernel, 3-4 % more per second at the 1.4 kW board power cap (DESIGN.md §3.1).
 
 Per wave and step j (the loop is unrolled over the 4 ring phases; slot offsets are immediates):
   unmasked  j+1 <= t_w, j+1 < e_w : M(j), V(j)
@@ -27,6 +27,12 @@ Softmax without a row max in the loop (the 4-wave kernel's scheme): P = exp2(S c
 m = the masked max of tile 0; a V phase whose partial row sums pass 2^slack takes the rare path
 (true max, O and l rescaled, softmax redone).
 
+FEATURES (round 6): softcap and ALiBi in an out-of-line pass over the tile's raw scores before
+its softmax (feature_block; tile 0 before its max, the ALiBi max lifted by the row's best bias).
+LEFTWIN: the key test is two-sided per lane, (off - LIML) <u wid; tiles before %[lw] take the
+masked step; a row with no visible key in tile 0 starts from m = +inf, so its first visible key
+sends the tile down the rare path, which takes the true max.
+
 Register map (per lane, 256 = v[0:127] + a[0:127]):
   a[0:63]    O^T accumulators (4 d tiles x 16)
   a[64:95]   Q fragments (8 x 4), the B operand of S^T = K Q^T
@@ -36,6 +42,7 @@ Register map (per lane, 256 = v[0:127] + a[0:127]):
   v[48:55]   softmax scratch (epilogue / redo temps)
   v56 tile row sum, v57 -m, v58 running row sum, v59 key limit, v60-63 redo / first-max temps
   v[64:95]   V^T fragment ring (8 slots x 4)
+  v96 the left key limit (LEFTWIN, stepped with v59), v97 its compare temp
   s[80:87]   DMA descriptors (K, V) of the next tile to load; s88 step, s89 temp, s90 stored,
   s[92:93]   return address, s[94:95] compare mask
 

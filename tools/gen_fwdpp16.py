@@ -1,5 +1,5 @@
 """Generate csrc/fmha_fwdpp16_body.h: the 8-wave ping-pong D = 128 forward body on the bf16 /
-f16 MFMA shape v_mfma_f32_16x16x32 (csrc/fmha_fwdpp_kernel.h with M16; DESIGN.md 3.1d).
+f16 MFMA shape v_mfma_f32_16x16x32 (csrc/fmha_fwdpp_kernel.h with M16; DESIGN.md §3.1).
 
 The phase program of tools/gen_fwdpp.py (read its docstring: two waves per SIMD, waves 4-7 one
 phase behind waves 0-3, MFMA phases PV(j) + QK^T(j+1) against VALU phases softmax(j+1) +

@@ -2,7 +2,7 @@
 
 NOT part of the product.  It answers one question with a measurement: does a second wave per
 SIMD, running its LDS-DMA issue and softmax VALU while its partner issues MFMAs, beat the
-4-wave kernel (one wave per SIMD, everything on one instruction stream, DESIGN.md 3.1b)?
+4-wave kernel (one wave per SIMD, everything on one instruction stream, DESIGN.md appendix A.1)?
 
 Structure (tools/probe/pingpong.hip wraps the generated item body):
   * workgroup = 8 waves x 32 query rows = 256 rows (the 4-wave kernel's item), waves w and w+4

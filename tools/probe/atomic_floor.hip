@@ -1,4 +1,4 @@
-// The dQ-atomic floor of the C3 backward, measured (DESIGN.md 3.2; VERDICT r4 item 3).
+// The dQ-atomic floor of the C3 backward, measured (DESIGN.md §3.3; VERDICT r4 item 3).
 //
 // The backward's main kernel adds every key block's dQ tile into the fp32 accumulator with float
 // atomics (csrc/fmha_bwd_kernel.h; the reference does the same, flash_bwd_kernel_hip.h:637).

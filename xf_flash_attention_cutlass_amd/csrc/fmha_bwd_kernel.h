@@ -18,9 +18,12 @@
 //    all waves and added to an fp32 dQ accumulator with global float atomics (256 keys per
 //    workgroup => 640 MFMA flops per atomic byte, cdna_hip_programming.md Appendix B), or, in
 //    deterministic mode, into one of S = ceil(CUs / (b * hk)) accumulator slices (the bound of
-//    export.cpp:1090-1091): workgroup (bh, s) walks key blocks s, s + S, s + 2S, ... in order,
-//    retiring each block's atomics before the next, and the convert kernel sums the slices in
-//    order - bitwise reproducible, workspace independent of seqlen_k;
+//    export.cpp:1090-1091): workgroup (bh, s) is the slice's only writer and walks key blocks
+//    s, s + S, s + 2S, ... in order (snake order over rounds), so it adds its dQ tiles by plain
+//    read-modify-write (16-byte loads and stores, D <= 128; its first block writes instead of
+//    adding, so the slices need no zeroing), retires each block's stores before the next, and
+//    the convert kernel sums the slices in order - bitwise reproducible, workspace independent
+//    of seqlen_k;
 //  * P is recomputed from the forward LSE; D = rowsum(dO*O) comes from the preprocess kernel.
 #pragma once
 

@@ -162,7 +162,7 @@ static hipError_t launch_fwdpp(const FwdParams& p, hipStream_t st) {
     constexpr bool BF = std::is_same<elem_t, __bf16>::value;
     // fwd_w4 = 3: the body on the 16x16x32 MFMA shape (tools/gen_fwdpp16.py); 4 (auto, the
     // default): 16x16x32 where no row has a right window (causal / local rows: 32x32x16), the
-    // faster of the two per mask on the same box (DESIGN.md 3.1d)
+    // faster of the two per mask on the same box (DESIGN.md §3.1)
     const bool m16 = p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0 && !p.alibi && !(p.softcap_pre > 0.f));
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] {

@@ -12,7 +12,7 @@
 //    MFMA gap by tools/gen_fwd4.py;
 //  * no row max in the loop: P = exp2(S c - m) against the first tile's true row max; a tile
 //    whose partial row sums pass 2^fwd_slack re-runs its softmax against the true running max
-//    after rescaling O and l (rare; same result up to rounding, DESIGN.md 3.1);
+//    after rescaling O and l (rare; same result up to rounding, DESIGN.md §3.1);
 //  * K / V tiles arrive by LDS-DMA into 4-slot K and V rings: step j issues K_{j+4} and V_{j+2}
 //    and publishes K_{j+3}, V_{j+1} at its mid-point barrier (one barrier per tile).
 //

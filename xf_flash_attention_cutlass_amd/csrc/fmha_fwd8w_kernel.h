@@ -17,6 +17,18 @@
 
 namespace xfa {
 
+#ifdef XFA_FWD8_STAMPS
+// Diagnostic build only (gen_fwd8.py --stamps, read by tools/fwd8_stamps.py): each wave sums
+// the s_memtime cycles per phase class in lanes 0..7 of one register; the kernel adds them into
+// this array at its end (read by fmha_fwd8_stamps).
+static __device__ unsigned g_fwd8_stamps[4 * 8];
+#define XFA_F8_ACC_PARAM , unsigned& acc
+#define XFA_F8_ACC_ARG , acc
+#else
+#define XFA_F8_ACC_PARAM
+#define XFA_F8_ACC_ARG
+#endif
+
 constexpr int kFwd8wRows = 256;            // query rows per workgroup (4 waves x 64)
 constexpr int kFwd8wTile = 64 * 128;       // bytes of one fp8 K (or V) tile
 constexpr int kFwd8wVReg = 4 * kFwd8wTile; // V ring after the 4 K slots
@@ -42,7 +54,7 @@ __device__ __forceinline__ int v8w_off(int row, int chunk) { return row * 128 + 
 
 // One (batch x kv head, 256-row query block) item.
 template <bool F16>
-__device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const int bh, const int m_block) {
+__device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const int bh, const int m_block XFA_F8_ACC_PARAM) {
     constexpr int HD = 128;
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));        // item-local (see fmha_fwd4_kernel.h)
@@ -152,11 +164,11 @@ __device__ __forceinline__ void fwd8w_item(const FwdParams& p, char* smem, const
     if constexpr (F16)
         fwd8_item_f16(kblo, kbhi, vblo, vbhi, (int)kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w,
                       c, thr, p.v_scale, ka[0], ka[1], ka[2], ka[3], va[0], va[1], va[2], va[3], dk[0], dk[1],
-                      dv[0], dv[1], lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]);
+                      dv[0], dv[1], lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1] XFA_F8_ACC_ARG);
     else
         fwd8_item_bf16(kblo, kbhi, vblo, vbhi, (int)kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w,
                        c, thr, p.v_scale, ka[0], ka[1], ka[2], ka[3], va[0], va[1], va[2], va[3], dk[0], dk[1],
-                       dv[0], dv[1], lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1]);
+                       dv[0], dv[1], lim[0], lim[1], qoff[0], qoff[1], ooff[0], ooff[1], loff[0], loff[1] XFA_F8_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU): XCD-grouped (n-1-i, i) row-block pairs, or (fwd_dyn
@@ -167,6 +179,9 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd8w_kernel(const FwdParams p) {
     __shared__ int s_claim[2];
     const int nbh = p.b * p.hk;
     const int g = gridDim.x;
+#ifdef XFA_FWD8_STAMPS
+    unsigned acc = 0;
+#endif
     for (int k = 0;; ++k) {
         int bh, m_block;
         if (p.persistent == 3) {
@@ -203,8 +218,11 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd8w_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
-        fwd8w_item<F16>(p, smem, bh, m_block);
+        fwd8w_item<F16>(p, smem, bh, m_block XFA_F8_ACC_ARG);
     }
+#ifdef XFA_FWD8_STAMPS
+    if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwd8_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], acc);
+#endif
     if (p.persistent == 3 && threadIdx.x == 0) {
         // the grid's last workgroup resets the queue counters for the next launch on the stream
         const int total = (int)(gridDim.x * gridDim.y * gridDim.z);

@@ -1,5 +1,5 @@
 // fmha_fwdpp_kernel.h — 8-wave "ping-pong" forward for D = 128 (two waves per SIMD, 32 query
-// rows per wave; DESIGN.md 3.1c).
+// rows per wave; DESIGN.md §3.1).
 //
 // Replaces the reference's `compute_attn_1rowblock_splitkv` (flash_fwd_kernel_hip.h:585-1283)
 // for the shapes the 4-wave kernel (fmha_fwd4_kernel.h) runs — dense and varlen, D = 128, bf16 /
