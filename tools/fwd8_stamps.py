@@ -30,19 +30,24 @@ def main():
     from xf_flash_attention_cutlass_amd import capi
     lib = capi.load(a.lib, strict=False)
     st = ctypes.CDLL(a.lib).fmha_fwd8_stamps
-    st.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
+    st.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     b, h, s, d = 4, 32, 4096, 128
-    q, k, v = ((torch.randn(b, s, h, d, device="cuda") * 2).to(torch.float8_e4m3fn) for _ in range(3))
+    xs = []                                  # bench.py workload_fp8's inputs: N(0, 1), scaled
+    for _ in range(3):
+        t = torch.randn(b, s, h, d, device="cuda")
+        sc = float(t.abs().max()) / 448.0
+        xs.append(((t / sc).to(torch.float8_e4m3fn), sc))
+    (q, qs), (k, ks), (v, vs) = xs
     o = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(b, h, s, device="cuda", dtype=torch.float32)
     P = lambda t: t.data_ptr()  # noqa: E731
     stream = torch.cuda.current_stream().cuda_stream
-    buf = (ctypes.c_uint * 32)()
+    buf = (ctypes.c_ulonglong * 32)()
     for causal in (True, False):
         wr = 0 if causal else -1
 
         def run():
-            lib.fmha_fwd_fp8(P(q), P(k), P(v), P(o), P(lse), 1.0, 1.0, 1.0, s, s, b, h, h, d, d ** -0.5,
+            lib.fmha_fwd_fp8(P(q), P(k), P(v), P(o), P(lse), qs, ks, vs, s, s, b, h, h, d, d ** -0.5,
                              -1, wr, False, stream)
         for _ in range(5):
             run()

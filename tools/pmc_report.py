@@ -115,7 +115,10 @@ def main():
                 e["profiled_duration_us"] = round(dur / 1e3, 2)
                 e["effective_clock_ghz"] = round(cyc / dur, 3) if long_enough else None
             if long_enough and "SQ_INSTS_MFMA" in c:
-                per = 64 if "fp8" in k or "fwd8" in k else 32
+                # cycles per MFMA instruction: 64 for the block-scaled fp8 one, 16 for
+                # v_mfma_f32_16x16x32 (the M16 ping-pong body, the 16-row decode tile), else 32
+                m16 = "fmha_fwdpp_kernel<true, true>" in k or "fmha_fwdpp_kernel<false, true>" in k
+                per = 64 if "fp8" in k or "fwd8" in k else 16 if (m16 or "decode" in k) else 32
                 e["mfma_util_from_insts"] = round(c["SQ_INSTS_MFMA"] * per / (4 * NUM_CUS * cyc), 4)
             if c.get("SQ_INSTS_MFMA"):
                 e["valu_per_mfma"] = round(c.get("SQ_INSTS_VALU", 0) / c["SQ_INSTS_MFMA"], 2)

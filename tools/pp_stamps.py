@@ -22,7 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--noncausal", action="store_true")
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=3,
+                    help="launches summed (the device counters are 32-bit: keep 256 CUs x launches x cycles < 2^32)")
     a = ap.parse_args()
     from xf_flash_attention_cutlass_amd import capi
     lib = capi.load(a.lib, strict=False)

@@ -21,7 +21,7 @@ namespace xfa {
 // Diagnostic build only (gen_fwd8.py --stamps, read by tools/fwd8_stamps.py): each wave sums
 // the s_memtime cycles per phase class in lanes 0..7 of one register; the kernel adds them into
 // this array at its end (read by fmha_fwd8_stamps).
-static __device__ unsigned g_fwd8_stamps[4 * 8];
+static __device__ unsigned long long g_fwd8_stamps[4 * 8];   // (64-bit: 256 workgroups x launches)
 #define XFA_F8_ACC_PARAM , unsigned& acc
 #define XFA_F8_ACC_ARG , acc
 #else
@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256, 1) fmha_fwd8w_kernel(const FwdParams p) {
         fwd8w_item<F16>(p, smem, bh, m_block XFA_F8_ACC_ARG);
     }
 #ifdef XFA_FWD8_STAMPS
-    if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwd8_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], acc);
+    if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwd8_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], (unsigned long long)acc);
 #endif
     if (p.persistent == 3 && threadIdx.x == 0) {
         // the grid's last workgroup resets the queue counters for the next launch on the stream

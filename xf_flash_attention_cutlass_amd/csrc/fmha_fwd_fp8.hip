@@ -98,11 +98,11 @@ hipError_t launch_fwd_fp8(const FwdParams& p, bool out_fp16, hipStream_t st) {
 
 #ifdef XFA_FWD8_STAMPS
 // diagnostic builds only: copy out (and optionally clear) the 4-wave fp8 phase stamps
-extern "C" int fmha_fwd8_stamps(unsigned* out, int reset) {
+extern "C" int fmha_fwd8_stamps(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(xfa::g_fwd8_stamps), sizeof(xfa::g_fwd8_stamps)) != hipSuccess) return -1;
     if (reset) {
-        unsigned zero[4 * 8] = {};
+        unsigned long long zero[4 * 8] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(xfa::g_fwd8_stamps), zero, sizeof(zero)) != hipSuccess) return -1;
     }
     return 0;
