@@ -368,3 +368,73 @@ def test_fwdpp_alibi_softcap(b, h, hk, sq, sk, causal, window, alibi, softcap, d
     assert torch.equal(torch.isinf(lse), ~fin)
     assert (lse[fin] - lref[fin]).abs().max().item() < 1e-3
     assert (o.float() - o8.float()).abs().max().item() <= 4 * (pt.float() - ref).abs().max().item() + 1e-2
+
+
+@pytest.mark.parametrize("window,alibi", [((127, 0), True), ((300, 40), False), ((0, 0), False)])
+def test_fwdpp_varlen_left_window(window, alibi):
+    """Left windows on ragged varlen sequences through the ping-pong kernel (each sequence's item
+    key range starts at its first row's window: the per-sequence T0 shift), with ALiBi; O per
+    sequence against the oracle (test.py:975 rule), LSE against the fp32 log-sum-exp"""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    g = torch.Generator().manual_seed(11 + window[0])
+    lens = [1, 65, 300, 700, 129, 513]
+    h, hk = 4, 2
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32)
+    tot = int(cu[-1])
+    q = (torch.randn(tot, h, 128, generator=g) * 2).bfloat16()
+    k, v = (torch.randn(tot, hk, 128, generator=g).bfloat16() for _ in range(2))
+    slopes = torch.rand(len(lens), h, generator=g) * 0.3 if alibi else None
+    out, lse, _ = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV), cu.to(DEV),
+                                             max(lens), max(lens), window_size=window,
+                                             alibi_slopes=slopes.to(DEV) if alibi else None,
+                                             return_attn_probs=True)
+    torch.cuda.synchronize()
+    kern = capi.lib().fmha_last_kernel().decode()
+    if capi.lib().fmha_get_option(b"fwd_w4") in (2, 4):
+        assert kern.startswith("fmha_fwdpp_kernel "), kern
+    out, lse = out.cpu(), lse.cpu()
+    for i, n in enumerate(lens):
+        a, e = int(cu[i]), int(cu[i + 1])
+        qs, ks, vs = q[a:e][None], k[a:e][None], v[a:e][None]
+        s = slopes[i:i + 1] if alibi else None
+        bias = orc.alibi_bias(s, n, n, causal=False) if alibi else None
+        ref, _ = orc.attention_ref(qs, ks, vs, attn_bias=bias, window_size=window)
+        pt, _ = orc.attention_ref(qs, ks, vs, attn_bias=bias, window_size=window, upcast=False,
+                                  reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[a:e][None].float(), ref, pt, 2.0, 1e-5)
+        assert ok, f"seq {i} (len {n}): {err:.3g} > {bound:.3g}"
+        lref = orc.attention_lse_ref(qs, ks, attn_bias=bias, window_size=window)[0]
+        fin = torch.isfinite(lref)
+        assert torch.equal(torch.isinf(lse[:, a:e]), ~fin)
+        assert (lse[:, a:e][fin] - lref[fin]).abs().max().item() < 1e-3
+
+
+def test_fwdpp_left_window_persistent_schedules():
+    """A sliding window over more items than CUs (B4 H16 S2048, window (255, 0): 512 items):
+    sampled heads against the oracle, every head bit-identical between the persistent XCD-paired
+    grid, one workgroup per item and the per-XCD dynamic queues (ring slots reused across items
+    with the item key range shifted per item)"""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    B, S, H, W = 4, 2048, 16, (255, 0)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    q, k, v = (torch.randn(B, S, H, 128, device=DEV, generator=g, dtype=torch.bfloat16) for _ in range(3))
+    out = xfa.flash_attn_func(q, k, v, window_size=W)
+    kern = L.fmha_last_kernel().decode()
+    if L.fmha_get_option(b"fwd_w4") in (2, 4):
+        assert kern.startswith("fmha_fwdpp_kernel persistent="), kern
+    for b, hh in ((0, 0), (2, 7), (3, 15)):
+        qs, ks, vs = (x[b:b + 1, :, hh:hh + 1].cpu() for x in (q, k, v))
+        ref, _ = orc.attention_ref(qs, ks, vs, window_size=W)
+        pt, _ = orc.attention_ref(qs, ks, vs, window_size=W, upcast=False, reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[b:b + 1, :, hh:hh + 1].cpu().float(), ref, pt, 2.0)
+        assert ok, f"b{b} h{hh}: {err:.3g} > {bound:.3g}"
+    for opt, val in ((b"fwd_persistent", 0), (b"fwd_dyn", 2)):
+        old = L.fmha_get_option(opt)
+        assert L.fmha_set_option(opt, val) == 0
+        try:
+            assert torch.equal(out, xfa.flash_attn_func(q, k, v, window_size=W)), opt
+        finally:
+            L.fmha_set_option(opt, old)
