@@ -58,6 +58,13 @@ __device__ __forceinline__ i32x4 fwdpp_srd(const void* base, uint32_t bytes) {
     return r;
 }
 
+// The 16x16x32 body's image: kv_off with the chunk XORed by ppx16(row bits 2-3) = 0, 2, 3, 1
+// instead of the bits themselves.  Its K row reads (16 lanes of a ds_read_b128 bank group cover
+// rows {0-3, 12-15} at one chunk and rows {4-11} at the next) and its V^T reads (rows 4 g + q of
+// lane group g) then land on distinct banks: 4 / 2 cycles instead of 8 / 4 (tools/fwdpp_banks.py;
+// PMC r06: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.5 with the plain image)
+__device__ __forceinline__ constexpr int ppx16(int x) { return (0x78 >> (2 * x)) & 3; }
+
 // One (batch x kv head, 256-row query block) item.  M16: the body on the 16x16x32 MFMA shape
 // (a lane holds rows l16 and 16 + l16 of its wave's 32; per-lane operands below).
 template <bool BF16, bool M16>
@@ -161,8 +168,10 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
 
     // LDS-DMA: wave w loads 8-row block w of every K / V tile, pieces i = chunks 8i .. 8i+7 of
     // the kv_off image (lane l lands at +16 l); K and V share the offsets (k_row == v_row)
+    // (M16: the chunk XOR by row bits 2-3 goes through ppx16, so the 16x16x32 body's K row and
+    // V^T reads are conflict-free too; see ppx16)
     const int r = 8 * wave + lr / 4;
-    const int cch = 4 * hh + ((lane & 3) ^ ((r >> 2) & 3));
+    const int cch = 4 * hh + ((lane & 3) ^ (M16 ? ppx16((r >> 2) & 3) : ((r >> 2) & 3)));
     const int dma0 = r * k_row * 2 + cch * 16;
     // LDS read bases (kv_off image, slot 0; the ring slots are immediate offsets)
     const int sbase = (int)(size_t)smem;
@@ -199,13 +208,13 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
         }
         // K row reads: key 16 kt + l16, chunk 4 s + g; V^T reads: lane 4 q + p of group g, key
         // 4 g + q (+ 32 ks + 16 h), d 16 dt + 4 p, base per dt parity e (kv_off image)
-        const int kb0 = sbase + 2048 * ((lane >> 3) & 1) + 64 * (lane & 7) + 16 * (g ^ ((lane >> 2) & 3));
+        const int kb0 = sbase + 2048 * ((lane >> 3) & 1) + 64 * (lane & 7) + 16 * (g ^ ppx16((lane >> 2) & 3));
         const int q4 = (lane & 15) >> 2, p4 = lane & 3;
         int vb16[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e)
             vb16[e] = sbase + kFwdppVReg + 2048 * (g >> 1) + 64 * (4 * (g & 1) + q4) +
-                      16 * ((2 * e + (p4 >> 1)) ^ g) + 8 * (p4 & 1);
+                      16 * ((2 * e + (p4 >> 1)) ^ ppx16(g)) + 8 * (p4 & 1);
 #ifdef XFA_FWDPP16_STAMPS
 #define XFA_PP16_ACC_ARG , acc
 #else
