@@ -22,12 +22,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--w4", type=int, default=2, help="fwd_w4: 2 the 32x32x16 body, 3 the 16x16x32 body")
     ap.add_argument("--iters", type=int, default=3,
                     help="launches summed (the device counters are 32-bit: keep 256 CUs x launches x cycles < 2^32)")
     a = ap.parse_args()
     from xf_flash_attention_cutlass_amd import capi
     lib = capi.load(a.lib, strict=False)
-    assert lib.fmha_set_option(b"fwd_w4", 2) == 0
+    assert lib.fmha_set_option(b"fwd_w4", a.w4) == 0
     st = ctypes.CDLL(a.lib).fmha_fwdpp_stamps
     st.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
     b, h, s, d = 4, 32, 4096, 128
