@@ -438,3 +438,32 @@ def test_fwdpp_left_window_persistent_schedules():
             assert torch.equal(out, xfa.flash_attn_func(q, k, v, window_size=W)), opt
         finally:
             L.fmha_set_option(opt, old)
+
+
+def test_fwdpp16_noncausal_dynamic_default():
+    """Dense non-causal D = 128 launches with more items than CUs run the 16x16x32 body from the
+    per-XCD dynamic queues by default (fwd_dyn = 1): sampled heads against the oracle, every head
+    bit-identical to the static XCD pairs (fwd_dyn = 0) and to one workgroup per item"""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    B, S, H = 4, 2048, 16
+    g = torch.Generator(device=DEV).manual_seed(8)
+    q, k, v = (torch.randn(B, S, H, 128, device=DEV, generator=g, dtype=torch.bfloat16) for _ in range(3))
+    out = xfa.flash_attn_func(q, k, v)
+    kern = L.fmha_last_kernel().decode()
+    if L.fmha_get_option(b"fwd_w4") == 4 and L.fmha_get_option(b"fwd_dyn") == 1:
+        assert kern.startswith("fmha_fwdpp16_kernel persistent=3 xcdq=1"), kern
+    for b, hh in ((0, 0), (3, 15)):
+        qs, ks, vs = (x[b:b + 1, :, hh:hh + 1].cpu() for x in (q, k, v))
+        ref, _ = orc.attention_ref(qs, ks, vs)
+        pt, _ = orc.attention_ref(qs, ks, vs, upcast=False, reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[b:b + 1, :, hh:hh + 1].cpu().float(), ref, pt, 2.0)
+        assert ok, f"b{b} h{hh}: {err:.3g} > {bound:.3g}"
+    for opt, val in ((b"fwd_dyn", 0), (b"fwd_persistent", 0)):
+        old = L.fmha_get_option(opt)
+        assert L.fmha_set_option(opt, val) == 0
+        try:
+            assert torch.equal(out, xfa.flash_attn_func(q, k, v)), opt
+        finally:
+            L.fmha_set_option(opt, old)
