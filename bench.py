@@ -560,6 +560,20 @@ def prewarm(step, seconds, sync):
         sync()
 
 
+def traffic_key(a, mode):
+    """the tools/pmc_round.sh mode whose measured HBM bytes belong to this run's kernel"""
+    if mode == "decode":
+        return "decode_ragged" if a.ragged else "decode"
+    if mode == "fwd":
+        if getattr(a, "alibi", False):
+            return "fwd_alibi"
+        if getattr(a, "window_left", -1) >= 0:
+            return "fwd_window"
+        if a.no_causal:
+            return "fwd_nc"
+    return mode
+
+
 def roofline(w, ev, mode):
     ms, ms_min, ms_max = ev
     hbm = w["bound"] == "hbm"
@@ -601,7 +615,7 @@ def sub_result(a, mode, dev, stream, **over):
     out = {"workload": w["config"]["workload"], "steps": k, "ms_per_step": round(wall_ms, 4),
            "value": round(w["units"] / (wall_ms / 1e3) / u, 2),
            "unit": "GB/s" if hbm else "TFLOP/s",
-           "roofline": roofline(w, ev, getattr(a, "roof_key", None) or mode + ("_ragged" if a.ragged else "")),
+           "roofline": roofline(w, ev, getattr(a, "roof_key", None) or traffic_key(a, mode)),
            "kernel": last_kernel(),
            "gpu_clock": clock_stats(t_pw + 0.2, t_end)}
     if not a.no_cpu_baseline:
@@ -794,7 +808,7 @@ def run(a, world, rank, local):
         # with the two masks the reference's kernel also takes, causal ALiBi and a causal
         # 1024-key sliding window (no CPU baselines for these three)
         extras["fwd_noncausal"] = sub_result(a, "fwd", dev, stream, no_causal=True,
-                                             no_cpu_baseline=True, roof_key="fwd_noncausal")
+                                             no_cpu_baseline=True, roof_key="fwd_nc")
         extras["fwd_alibi"] = sub_result(a, "fwd", dev, stream, alibi=True, no_cpu_baseline=True,
                                          roof_key="fwd_alibi")
         extras["fwd_window"] = sub_result(a, "fwd", dev, stream, window_left=1023,

@@ -31,7 +31,9 @@ FEATURES (round 6): softcap and ALiBi in an out-of-line pass over the tile's raw
 its softmax (feature_block; tile 0 before its max, the ALiBi max lifted by the row's best bias).
 LEFTWIN: the key test is two-sided per lane, (off - LIML) <u wid; tiles before %[lw] take the
 masked step; a row with no visible key in tile 0 starts from m = +inf, so its first visible key
-sends the tile down the rare path, which takes the true max.
+sends the tile down the rare path, which takes the true max.  A step whose tile
+j+1 lies before %[fw] (the wave's first tile with a visible key) is an idle step: tile 0's P of
+such a wave is all zero and stays in the P registers until step fw - 1, whose PV adds nothing.
 
 Register map (per lane, 256 = v[0:127] + a[0:127]):
   a[0:63]    O^T accumulators (4 d tiles x 16)
@@ -505,8 +507,10 @@ def group_program(dt, grp):
         vslot = (ph + DLEAD) % RING                          # the tile j+DLEAD this V phase loads
         out.append(f".Lph{ph}_{uid}:")
         out += st(ST_VW) + [f"s_cmp_ge_i32 s{SJ}, %[tw]", f"s_cbranch_scc1 .Lx{ph}_{uid}",
-                f"s_add_i32 s{ST}, s{SJ}, 1", f"s_cmp_lt_i32 s{ST}, %[ew]",
-                f"s_cbranch_scc0 .Lm{ph}_{uid}"]
+                f"s_add_i32 s{ST}, s{SJ}, 1"]
+        if LEFTWIN:   # tile j+1 before the wave's first visible tile: an idle step (P(j) = 0)
+            out += [f"s_cmp_lt_i32 s{ST}, %[fw]", f"s_cbranch_scc1 .Li{ph}_{uid}"]
+        out += [f"s_cmp_lt_i32 s{ST}, %[ew]", f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         if LEFTWIN:   # tiles before lw cross some row's left window edge
             out += [f"s_cmp_ge_i32 s{ST}, %[lw]", f"s_cbranch_scc0 .Lm{ph}_{uid}"]
         # unmasked step (inline)
@@ -573,7 +577,7 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
        "const int lim, const int qoff, const int ooff, const int loff, const int feat, "
        "const float scp2, const float alw, const float ald, const float alm, const int lw, "
-       "const int liml, const int wid")
+       "const int liml, const int wid, const int fw")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
@@ -582,7 +586,7 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[dma0] "v"(dma0)', '[dma1] "v"(dma1)', '[lim] "v"(lim)', '[qoff] "v"(qoff)',
        '[ooff] "v"(ooff)', '[loff] "v"(loff)', '[feat] "s"(feat)', '[scp2] "s"(scp2)',
        '[alw] "v"(alw)', '[ald] "v"(ald)', '[alm] "v"(alm)', '[lw] "s"(lw)', '[liml] "v"(liml)',
-       '[wid] "v"(wid)']
+       '[wid] "v"(wid)', '[fw] "s"(fw)']
 
 
 def clobbers():

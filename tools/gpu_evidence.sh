@@ -9,4 +9,4 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" >> gpurun_o
 tail -2 gpurun_out/gpu_suite.log
 bash tools/lease_ab.sh ${tag} || exit 1
 rm -rf gpurun_out/prof
-bash tools/pmc_round.sh fwd fwd_nc fwdbwd varlen decode decode_ragged fwd_fp8
+bash tools/pmc_round.sh fwd fwd_nc fwd_alibi fwd_window fwdbwd varlen decode decode_ragged fwd_fp8

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--s", type=int, default=4096)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--wl", type=int, default=-1, help="fwd: left window (with causal: a sliding window)")
     a = ap.parse_args()
 
     from xf_flash_attention_cutlass_amd import capi
@@ -104,7 +105,7 @@ def main():
                              hk, a.d, sc, -1, wr, False, stream)
             return
         lib.fmha_fwd(P(q), P(k), P(v), P(o), None, a.s, a.s, a.b, a.h, hk, a.d, 0.0, stream, None,
-                     sc, None, P(lse), -1, wr, 0.0, False, False, 0)
+                     sc, None, P(lse), a.wl, wr, 0.0, False, False, 0)
         if a.mode == "bwd":
             lib.fmha_bwd(P(do), P(q), P(k), P(v), P(o), P(lse), P(dq), P(dk), P(dv), None, None,
                          a.s, a.s, a.b, a.h, hk, a.d, 0.0, sc, -1, wr, 0.0, det, False, stream,

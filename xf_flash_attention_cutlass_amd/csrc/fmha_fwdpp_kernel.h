@@ -104,7 +104,7 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     // this wave: rows wrow0 .. wrow0 + 31; last tile t_w; tiles >= e_w need the right edge mask,
     // tiles < l_w the left one
     const int wrow0 = row0 + 32 * wave;
-    int t_w = -1, e_w = 1 << 30, l_w = 0;
+    int t_w = -1, e_w = 1 << 30, l_w = 0, f_w = 0;
     if (wrow0 < rows_total && ntl > 0) {
         const int wp_lo = wrow0 / G, wp_hi = (min(wrow0 + 32, rows_total) - 1) / G;
         const int lr_hi = lim_r(wp_hi), lr_lo = lim_r(wp_lo);
@@ -112,10 +112,12 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
         t_w = max(t_w, -1);
         e_w = (lr_lo > 0 ? lr_lo / kBlockN : 0) - T0;
         l_w = (lim_l(wp_hi) + kBlockN - 1) / kBlockN - T0;
+        f_w = lim_l(wp_lo) / kBlockN - T0;     // tiles before it: no row of the wave sees a key
     }
     t_w = __builtin_amdgcn_readfirstlane(t_w);
     e_w = __builtin_amdgcn_readfirstlane(e_w);
     l_w = __builtin_amdgcn_readfirstlane(l_w);
+    f_w = __builtin_amdgcn_readfirstlane(f_w);
 
     // this lane's row
     const int row = wrow0 + lr;
@@ -245,11 +247,11 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        feat, scp2, alw, ald, alm, l_w, liml, wid XFA_PP_ACC_ARG);
+                        feat, scp2, alw, ald, alm, l_w, liml, wid, f_w XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                       feat, scp2, alw, ald, alm, l_w, liml, wid XFA_PP_ACC_ARG);
+                       feat, scp2, alw, ald, alm, l_w, liml, wid, f_w XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
