@@ -80,6 +80,9 @@ def parse(argv=None):
     ap.add_argument("--window-left", type=int, default=-1,
                     help="fwd/fwdbwd: left window (causal + wl = a sliding window of wl + 1 keys)")
     ap.add_argument("--ragged", action="store_true", help="decode: cache lengths U[1, S]")
+    ap.add_argument("--page", type=int, default=0,
+                    help="fwd: K/V in a paged cache of this page size (random-permutation block "
+                         "table; the reference's fmha_page_kvcache_fwd prefill)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="input sets cycled step by step (default: 2 for fwd/fwdbwd, so every "
                          "step reads inputs last touched two steps ago; C4/C5 inputs exceed the "
@@ -266,6 +269,28 @@ def workload_dense(a, mode, dev, rank, world):
         q, k, v, out, _ = nxt()
         res["r"] = pa.fwd(q, k, v, out, alibi, 0.0, scale, causal, wl, -1, 0.0, False, None)
 
+    page = getattr(a, "page", 0) if mode == "fwd" else 0
+    if page:
+        # the same K / V laid into paged caches (one random-permutation block table per set)
+        nbp = (S + page - 1) // page
+        paged_sets = []
+        for q, k, v, out, _ in sets:
+            table = torch.randperm(B * nbp, device=dev, generator=g).int().view(B, nbp)
+            kc = torch.zeros(B * nbp, page, Hr, D, device=dev, dtype=torch.bfloat16)
+            vc = torch.zeros_like(kc)
+            kc.view(-1, Hr, D)[(table.long().view(B, nbp, 1) * page +
+                                torch.arange(page, device=dev)).view(B, -1)[:, :S].reshape(-1)] = k.reshape(-1, Hr, D)
+            vc.view(-1, Hr, D)[(table.long().view(B, nbp, 1) * page +
+                                torch.arange(page, device=dev)).view(B, -1)[:, :S].reshape(-1)] = v.reshape(-1, Hr, D)
+            paged_sets.append((q, kc, vc, table))
+        seqlens = torch.full((B,), S, dtype=torch.int32, device=dev)
+        pnxt = _rotating(paged_sets)
+
+        def fwd():      # noqa: F811
+            q, kc, vc, table = pnxt()
+            res["r"] = pa.fwd_kvcache(q, kc, vc, None, None, seqlens, None, None, None, table, alibi,
+                                      None, scale, causal, wl, -1, 0.0, True, 1, None)
+
     def fwdbwd():
         q, k, v, out, dout = nxt()
         r = pa.fwd(q, k, v, out, alibi, 0.0, scale, causal, wl, -1, 0.0, False, None)
@@ -279,7 +304,8 @@ def workload_dense(a, mode, dev, rank, world):
         ff = 4.0 * B * Hr * D * vis
     mult = 3.5 if mode == "fwdbwd" else 1.0
     cs = ("causal" if causal else "non-causal") + (" ALiBi" if a.alibi else "") + \
-        (f" window ({wl}, {0 if causal else wl})" if wl >= 0 else "")
+        (f" window ({wl}, {0 if causal else wl})" if wl >= 0 else "") + \
+        (f", paged K/V (page {page}, random block table)" if page else "")
     glob_b = B * world if a.scaling == "weak" else B
     return dict(step=fwd if mode == "fwd" else fwdbwd, units=ff * mult, bound="mfma",
                 out=lambda: sets[0][3], gather_dim=0 if a.scaling == "weak" else 2,
@@ -569,6 +595,8 @@ def traffic_key(a, mode):
             return "fwd_alibi"
         if getattr(a, "window_left", -1) >= 0:
             return "fwd_window"
+        if getattr(a, "page", 0):
+            return "fwd_paged"
         if a.no_causal:
             return "fwd_nc"
     return mode
@@ -811,6 +839,8 @@ def run(a, world, rank, local):
                                              no_cpu_baseline=True, roof_key="fwd_nc")
         extras["fwd_alibi"] = sub_result(a, "fwd", dev, stream, alibi=True, no_cpu_baseline=True,
                                          roof_key="fwd_alibi")
+        extras["fwd_paged"] = sub_result(a, "fwd", dev, stream, page=16, no_cpu_baseline=True,
+                                         roof_key="fwd_paged")
         extras["fwd_window"] = sub_result(a, "fwd", dev, stream, window_left=1023,
                                           no_cpu_baseline=True, roof_key="fwd_window")
     if dist:

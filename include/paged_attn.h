@@ -139,9 +139,10 @@ const char* fmha_version(void);
  * query rows per forward workgroup), fwd_prio (0/1), fwd_persistent (workgroups per CU, 0 =
  * one workgroup per item), fwd_slack (0..16), fwd_order (0/1), fwd_dyn (0..2), fwd_xcdq (0/1),
  * fwd_pipe (0..2), fwd_decode (0/1), dec_wg_per_cu (1..16), dec_hmaj (0..2), dec_mr (16/32),
- * fwd_w4 (D = 128 forward where eligible: 4 auto, the default = 3 where no row has a right
- * window, else 2; 3 the 8-wave ping-pong kernel on the 16x16x32 MFMA; 2 the 8-wave ping-pong
- * kernel on 32x32x16; 1 the 4-wave kernel; 0 neither), fp8_w4 (fp8 forward: 1 the 4-wave kernel, the default; 2 the
+ * fwd_w4 (D = 128 forward where eligible — dense, varlen, or a paged cache whose page size is a
+ * power of two >= 8: 4 auto, the default = 3 where no row has a right window and the cache is
+ * not paged, else 2; 3 the 8-wave ping-pong kernel on the 16x16x32 MFMA (not paged); 2 the
+ * 8-wave ping-pong kernel on 32x32x16; 1 the 4-wave kernel (variants build); 0 neither), fp8_w4 (fp8 forward: 1 the 4-wave kernel, the default; 2 the
  * 8-wave ping-pong kernel; 0 the 8-wave compiler-scheduled one), comb_row (0/1), bwd_order (0/1),
  * bwd_desc (0/1), dec_fold (0/1: the decode split combine folded into the split launch). */
 int fmha_set_option(const char* name, int value);

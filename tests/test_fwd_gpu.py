@@ -337,9 +337,18 @@ def test_paged_fp8_cache(xfa, num_splits, sq, hk, dtype):
     out8, lse8 = xfa.flash_attn_with_kvcache(q, kp8.to(DEV), vp8.to(DEV), cache_seqlens=seqlens,
                                              block_table=tab, num_splits=num_splits,
                                              return_softmax_lse=True, k_scale=ks, v_scale=vs)
-    outd, lsed = xfa.flash_attn_with_kvcache(q, kpd.to(DEV), vpd.to(DEV), cache_seqlens=seqlens,
-                                             block_table=tab, num_splits=num_splits,
-                                             return_softmax_lse=True)
+    # (the 16-bit paged cache would run the ping-pong kernel: compare with the kernel the fp8
+    # cache runs, whose staging the bit-for-bit claim is about)
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    w4 = L.fmha_get_option(b"fwd_w4")
+    assert L.fmha_set_option(b"fwd_w4", 0) == 0
+    try:
+        outd, lsed = xfa.flash_attn_with_kvcache(q, kpd.to(DEV), vpd.to(DEV), cache_seqlens=seqlens,
+                                                 block_table=tab, num_splits=num_splits,
+                                                 return_softmax_lse=True)
+    finally:
+        L.fmha_set_option(b"fwd_w4", w4)
     if sq * h // hk > 32:
         assert torch.equal(out8, outd)
         assert torch.equal(lse8, lsed)

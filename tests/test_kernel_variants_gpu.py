@@ -467,3 +467,89 @@ def test_fwdpp16_noncausal_dynamic_default():
             assert torch.equal(out, xfa.flash_attn_func(q, k, v)), opt
         finally:
             L.fmha_set_option(opt, old)
+
+
+PAGED_CASES = [
+    # b, h, hk, sq, cache lens, page, causal, window, alibi
+    (2, 4, 4, 300, [300, 300], 16, True, (-1, -1), False),
+    (3, 8, 2, 129, [700, 129, 1000], 64, True, (-1, -1), False),     # chunked prefill: sq < sk
+    (2, 4, 2, 513, [513, 600], 256, False, (-1, -1), False),
+    (2, 4, 4, 400, [1100, 400], 32, False, (127, 0), True),          # sliding window + ALiBi
+    (1, 4, 4, 777, [777], 128, True, (-1, -1), True),
+    (2, 4, 4, 200, [200, 333], 48, True, (-1, -1), False),           # not a power of two: fallback
+]
+
+
+@pytest.mark.parametrize("b,h,hk,sq,lens,page,causal,window,alibi", PAGED_CASES)
+def test_fwdpp_paged_prefill(b, h, hk, sq, lens, page, causal, window, alibi):
+    """Paged-K/V prefill on the ping-pong kernel (gen_fwdpp.py PAGED: per tile each wave loads its
+    page id from the block table and builds its own descriptors): O and LSE against the oracle
+    per sequence, and bit-identical to the dense ping-pong kernel over the gathered cache (same
+    tiles, same arithmetic).  Page sizes that are not a power of two >= 8 take the
+    compiler-scheduled kernel."""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    g = torch.Generator().manual_seed(sq + page)
+    sk_max = max(lens)
+    nbp = (sk_max + page - 1) // page
+    q = (torch.randn(b, sq, h, 128, generator=g) * 2).bfloat16()
+    kf = torch.randn(b, nbp * page, hk, 128, generator=g).bfloat16()
+    vf = torch.randn(b, nbp * page, hk, 128, generator=g).bfloat16()
+    perm = torch.randperm(b * nbp, generator=g)
+    table = perm.view(b, nbp).int()
+    kc = torch.full((b * nbp, page, hk, 128), float("nan")).bfloat16()   # rows past a sequence: NaN
+    vc = torch.full((b * nbp, page, hk, 128), float("nan")).bfloat16()
+    for i in range(b):
+        n = lens[i]
+        for pi in range((n + page - 1) // page):
+            rows = min(page, n - pi * page)
+            kc[table[i, pi], :rows] = kf[i, pi * page:pi * page + rows]
+            vc[table[i, pi], :rows] = vf[i, pi * page:pi * page + rows]
+    slopes = torch.rand(b, h, generator=g) * 0.3 if alibi else None
+    seqlens = torch.tensor(lens, dtype=torch.int32)
+    out, lse = xfa.flash_attn_with_kvcache(q.to(DEV), kc.to(DEV), vc.to(DEV), cache_seqlens=seqlens.to(DEV),
+                                           block_table=table.to(DEV), causal=causal, window_size=window,
+                                           alibi_slopes=slopes.to(DEV) if alibi else None,
+                                           num_splits=1, return_softmax_lse=True)
+    torch.cuda.synchronize()
+    kern = L.fmha_last_kernel().decode()
+    pow2 = page >= 8 and page & (page - 1) == 0
+    if L.fmha_get_option(b"fwd_w4") in (2, 4):
+        want = "fmha_fwdpp_paged_kernel " if pow2 else "fmha_fwd_kernel"
+        assert kern.startswith(want), kern
+    out, lse = out.cpu(), lse.cpu()
+    w = (-1, 0) if causal else (window[0], max(lens)) if window[0] >= 0 and window[1] < 0 else window
+    for i in range(b):
+        n = lens[i]
+        qs, ks, vs = q[i:i + 1], kf[i:i + 1, :n], vf[i:i + 1, :n]
+        s = slopes[i:i + 1] if alibi else None
+        bias = orc.alibi_bias(s, sq, n, causal=causal) if alibi else None
+        ref, _ = orc.attention_ref(qs, ks, vs, attn_bias=bias, causal=causal, window_size=w)
+        pt, _ = orc.attention_ref(qs, ks, vs, attn_bias=bias, causal=causal, window_size=w, upcast=False,
+                                  reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[i:i + 1].float(), ref, pt, 2.0, 1e-5)
+        assert ok, f"seq {i}: {err:.3g} > {bound:.3g}"
+        bl = orc.alibi_bias_kernel(s, sq, n, causal=causal) if alibi else None
+        lref = orc.attention_lse_ref(qs, ks, attn_bias=bl, causal=causal, window_size=w)
+        fin = torch.isfinite(lref)
+        assert (lse[i:i + 1][fin] - lref[fin]).abs().max().item() < 1e-3
+        if pow2 and L.fmha_get_option(b"fwd_w4") in (2, 4):
+            # the dense ping-pong kernel (32x32 body) over the gathered rows: bit for bit
+            # (one split, as the paged launch above: the split heuristic would pick split-KV)
+            old = L.fmha_get_option(b"fwd_w4")
+            assert L.fmha_set_option(b"fwd_w4", 2) == 0
+            qd, kd, vd = (x.to(DEV).contiguous() for x in (qs, ks, vs))
+            od = torch.empty_like(qd)
+            sl = s.to(DEV).contiguous() if alibi else None
+            wl, wr = (-1, 0) if causal else w
+            try:
+                L.fmha_fwd(qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), od.data_ptr(),
+                           sl.data_ptr() if alibi else None, sq, n, 1, h, hk, 128, 0.0,
+                           capi.stream_handle(), None, 128 ** -0.5, None, None, wl, wr, 0.0, False, False, 1)
+                capi.check()
+                torch.cuda.synchronize()
+                assert L.fmha_last_kernel().decode().startswith("fmha_fwdpp_kernel ")
+            finally:
+                L.fmha_set_option(b"fwd_w4", old)
+            assert torch.equal(od.cpu(), out[i:i + 1]), f"seq {i}: paged != dense"

@@ -35,6 +35,12 @@ sends the tile down the rare path, which takes the true max.  
 j+1 lies before %[fw] (the wave's first tile with a visible key) is an idle step: tile 0's P of
 such a wave is all zero and stays in the P registers until step fw - 1, whose PV adds nothing.
 
+PAGED (fwdpp_pg_item_*): K / V in a paged cache.  A wave's DMA share of a tile (8 rows) lies in
+one page (power-of-two page size >= 8), so each wave builds its own descriptors per tile:
+pg_load at a V phase's start (the SMEM load of its next page id; nothing in a V phase waits on
+lgkmcnt for LDS reads before pg_compute retires it), pg_compute at its end (base = pool + page
+id x page stride + row in page x row bytes, range = its rows below the sequence length).
+
 Register map (per lane, 256 = v[0:127] + a[0:127]):
   a[0:63]    O^T accumulators (4 d tiles x 16)
   a[64:95]   Q fragments (8 x 4), the B operand of S^T = K Q^T
@@ -86,6 +92,8 @@ FEATURES = True        # the score features (softcap, ALiBi) behind %[feat] bits
 LEFTWIN = True         # two-sided key window in the masked steps (left windows: keys
                        # [LIML, LIML + %[wid]) of the tile, relative to this lane's offset 0)
 LIML, TW = 96, 97      # the lane's left key limit (stepped -64 per tile); a compare temp
+PAGED = False          # emitting the paged-K/V body (fwdpp_pg_item_*): per-wave page descriptors
+SKEY, SPG, ST2 = 91, 94, 95   # (paged) this wave's next key row to set up, its page id, a temp
 
 
 def addc_ret(reg, ret, pc, back):
@@ -210,7 +218,36 @@ def dma_pieces(slot):
     return out
 
 
+def pg_load():
+    """(paged) issue the page-id load of the tile whose descriptors pg_compute sets up next: this
+    wave's 8 rows from key SKEY (clamped to the last key, so the load stays in the sequence's
+    block-table row); an SMEM load, so it is issued at a V phase's start and waited for at its end
+    (no LDS read waits on lgkmcnt in between)"""
+    return [f"s_add_i32 s{ST}, %[skv], -1", f"s_min_i32 s{ST}, s{SKEY}, s{ST}",
+            f"s_lshr_b32 s{ST}, s{ST}, %[lgp]", f"s_lshl_b32 s{ST}, s{ST}, 2",
+            f"s_load_dword s{SPG}, %[btab], s{ST}"]
+
+
+def pg_compute():
+    """(paged) the K / V descriptors of this wave's 8 rows from key SKEY: base = pool + page id x
+    page stride + row in page x row bytes, range = its rows below the sequence length (rows past
+    it read zeros); then SKEY += 64"""
+    return ["s_waitcnt lgkmcnt(0)",
+            f"s_and_b32 s{ST}, s{SKEY}, %[pmask]", f"s_mul_i32 s{ST}, s{ST}, %[rowb]",
+            f"s_mul_hi_u32 s{ST2}, s{SPG}, %[pstr]", f"s_mul_i32 s{SPG}, s{SPG}, %[pstr]",
+            f"s_add_u32 s{SPG}, s{SPG}, s{ST}", f"s_addc_u32 s{ST2}, s{ST2}, 0",
+            f"s_add_u32 s{SKR}, %[kblo], s{SPG}", f"s_addc_u32 s{SKR + 1}, %[kbhi], s{ST2}",
+            f"s_and_b32 s{SKR + 1}, s{SKR + 1}, 0xffff",
+            f"s_add_u32 s{SVR}, %[vblo], s{SPG}", f"s_addc_u32 s{SVR + 1}, %[vbhi], s{ST2}",
+            f"s_and_b32 s{SVR + 1}, s{SVR + 1}, 0xffff",
+            f"s_sub_i32 s{ST}, %[skv], s{SKEY}", f"s_max_i32 s{ST}, s{ST}, 0", f"s_min_i32 s{ST}, s{ST}, 8",
+            f"s_mul_i32 s{SKR + 2}, s{ST}, %[rowb]", f"s_mov_b32 s{SVR + 2}, s{SKR + 2}",
+            f"s_add_u32 s{SKEY}, s{SKEY}, 64"]
+
+
 def dma_advance():
+    if PAGED:
+        return pg_compute()
     out = []
     for r in (SKR, SVR):
         out += [f"s_add_u32 s{r}, s{r}, %[kstep]", f"s_addc_u32 s{r + 1}, s{r + 1}, 0",
@@ -394,19 +431,20 @@ def v_phase(dt, slot, kind, uid, tag, feat=True):
     """V phase: kind 'u' unmasked softmax, 'm' masked, 'n' none; DMA of the tile in slot.
     Returns (inline, out-of-line stubs)."""
     pieces = dma_pieces(slot)
+    pre = pg_load() if PAGED else []
     if kind == "n" or ("nosm" in ABL and kind == "u"):
-        return sum(pieces, []) + dma_advance() + lim_step(), []
+        return pre + sum(pieces, []) + dma_advance() + lim_step(), []
     sm = softmax(dt, kind == "m")
     fin, fstub = feat_call(uid, tag) if feat else ([], [])
     if DMAMIX:
-        out = pieces[0] + VPH_NOPS                      # last QK^T results -> VALU
+        out = pre + pieces[0] + VPH_NOPS                # last QK^T results -> VALU
         # the other pieces spread through the softmax
         step = len(sm) // len(pieces)
         for n, pc in enumerate(pieces[1:]):
             at = (n + 1) * step + 3 * n
             sm[at:at] = pc
     else:
-        out = sum(pieces, []) + VPH_NOPS
+        out = pre + sum(pieces, []) + VPH_NOPS
     out += fin + sm
     inl, stub = redo_check(uid, tag)
     out += inl + dma_advance() + lim_step()
@@ -558,11 +596,16 @@ def item_program(dt):
     if not ABL & {"nopro", "nopq"}:
         out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
     out += [f"v_accvgpr_write_b32 a{ABASE_O + i}, 0" for i in range(64)]
-    for r, lo, hi in ((SKR, "kblo", "kbhi"), (SVR, "vblo", "vbhi")):
-        out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
-                f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
+    if PAGED:     # tile 0's descriptors from its page; later tiles' at each V phase's end
+        out += [f"s_mov_b32 s{SKR + 3}, 0x20000", f"s_mov_b32 s{SVR + 3}, 0x20000",
+                f"s_mov_b32 s{SKEY}, %[skey0]"] + pg_load() + pg_compute()
+    else:
+        for r, lo, hi in ((SKR, "kblo", "kbhi"), (SVR, "vblo", "vbhi")):
+            out += [f"s_mov_b32 s{r}, %[{lo}]", f"s_mov_b32 s{r + 1}, %[{hi}]",
+                    f"s_mov_b32 s{r + 2}, %[kvbytes]", f"s_mov_b32 s{r + 3}, 0x20000"]
     for slot in range(DLEAD - 1):                            # tiles 0 .. DLEAD-2
-        out += ([] if ABL & {"nopro", "nopkv"} else sum(dma_pieces(slot), [])) + dma_advance()
+        out += ([] if ABL & {"nopro", "nopkv"} else sum(dma_pieces(slot), []))
+        out += (pg_load() if PAGED else []) + dma_advance()
     # Q and tile 0 landed, published
     w = NPIECE * (DLEAD - 2) if not ABL & {"nopro", "nopkv"} else 0
     out += ([] if "nopro" in ABL else [f"s_waitcnt vmcnt({w})"]) + ["s_barrier"]
@@ -595,6 +638,11 @@ def clobbers():
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 
 
+SIG_PG = ", const int* btab, const int pstr, const int rowb, const int lgp, const int pmask, const int skv, const int skey0"
+OPS_PG = ['[btab] "s"(btab)', '[pstr] "s"(pstr)', '[rowb] "s"(rowb)', '[lgp] "s"(lgp)', '[pmask] "s"(pmask)',
+          '[skv] "s"(skv)', '[skey0] "s"(skey0)']
+
+
 def emit(out=OUT):
     lines = [
         "// GENERATED by tools/gen_fwdpp.py -- do not edit by hand.",
@@ -609,20 +657,24 @@ def emit(out=OUT):
         f"constexpr int kFwdppRing = {RING};           // K / V tile slots the body addresses",
         "",
     ]
-    for dt in ("bf16", "f16"):
+    global PAGED
+    # the dense body, then (not in stamps builds) the paged-K/V body
+    for paged, dt in [(False, "bf16"), (False, "f16")] + ([] if STAMPS else [(True, "bf16"), (True, "f16")]):
+        PAGED = paged
         prog = item_program(dt)
+        PAGED = False
         prog += GUARDS
         GUARDS.clear()
-        sig = SIG + (", unsigned& acc" if STAMPS else "")
-        lines.append(f"__device__ __forceinline__ void fwdpp_item_{dt}({sig}) {{")
+        sig = SIG + (SIG_PG if paged else "") + (", unsigned& acc" if STAMPS else "")
+        lines.append(f"__device__ __forceinline__ void fwdpp{'_pg' if paged else ''}_item_{dt}({sig}) {{")
         lines.append("    asm volatile(")
         lines += [f'        "{b}\\n"' for b in prog]
         lines.append('        : [acc] "+v"(acc)' if STAMPS else "        :")
-        lines.append("        : " + ",\n          ".join(OPS))
+        lines.append("        : " + ",\n          ".join(OPS + (OPS_PG if paged else [])))
         lines.append(f"        : {clobbers()});")
         lines.append("}")
         lines.append("")
-        print(dt, len(prog), "instructions/labels")
+        print(dt, "paged" if paged else "", len(prog), "instructions/labels")
     lines.append("}  // namespace xfa")
     open(out, "w").write("\n".join(lines) + "\n")
 

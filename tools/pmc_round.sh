@@ -10,7 +10,7 @@ mkdir -p gpurun_out/prof
 SQ1="SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 SQ2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
 for m in "$@"; do
-  case $m in decode_ragged) MA="--mode decode --ragged";; fwd_nc) MA="--mode fwd --no-causal";; fwd_alibi) MA="--mode fwd --alibi";; fwd_window) MA="--mode fwd --window-left 1023";; *) MA="--mode $m";; esac
+  case $m in decode_ragged) MA="--mode decode --ragged";; fwd_nc) MA="--mode fwd --no-causal";; fwd_paged) MA="--mode fwd --page 16";; fwd_alibi) MA="--mode fwd --alibi";; fwd_window) MA="--mode fwd --window-left 1023";; *) MA="--mode $m";; esac
   B="bench.py $MA --steps 10 --warmup 3 --no-cpu-baseline --no-extras --no-monitor --prewarm-s 0.5"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/${m}_stats -o run -- python3 $B > gpurun_out/prof/${m}_stats.out 2>&1 || { echo "FAILED stats $m"; exit 1; }
   echo "stats $m"

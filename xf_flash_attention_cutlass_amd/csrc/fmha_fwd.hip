@@ -139,10 +139,18 @@ static hipError_t launch_fwd_nw(const FwdParams& p, hipStream_t st) {
 // leftpad / dropout (those run the 8-wave kernel)
 // (ALiBi, softcap and left windows: the 32x32x16 ping-pong kernel only, its score-feature pass
 // and two-sided key window)
+// paged K/V on the ping-pong kernel (its 32x32x16 body): every 8-row block of a 64-key tile must
+// lie in one page (a power-of-two page size >= 8) and K and V must share their strides
+static bool fwdpp_paged_ok(const FwdParams& p) {
+    return p.page_size >= 8 && (p.page_size & (p.page_size - 1)) == 0 && p.k_batch == p.v_batch &&
+           (p.fwd4 == 2 || p.fwd4 == 4);
+}
+
 static bool fwd4_eligible(const FwdParams& p) {
     const bool feat = p.alibi || p.softcap_pre > 0.f || (p.wl >= 0 && p.wl < p.seqlen_k);
-    return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 && !p.block_table &&
-           !p.kv_fp8 && !p.leftpad_k && !p.drop && (!feat || p.fwd4 == 2 || p.fwd4 == 4);
+    return p.fwd4 && p.d == 128 && p.k_row == p.v_row && p.num_splits <= 1 &&
+           (!p.block_table || fwdpp_paged_ok(p)) && !p.kv_fp8 && !p.leftpad_k && !p.drop &&
+           (!feat || p.fwd4 == 2 || p.fwd4 == 4);
 }
 
 // 8-wave ping-pong forward (fmha_fwdpp_kernel.h): the same items, schedules and eligibility
@@ -163,14 +171,18 @@ static hipError_t launch_fwdpp(const FwdParams& p, hipStream_t st) {
     // fwd_w4 = 3: the body on the 16x16x32 MFMA shape (tools/gen_fwdpp16.py); 4 (auto, the
     // default): 16x16x32 where no row has a right window (causal / local rows: 32x32x16), the
     // faster of the two per mask on the same box
-    const bool m16 = p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0 && !p.alibi && !(p.softcap_pre > 0.f));
+    const bool m16 = !p.block_table &&
+                     (p.fwd4 == 3 || (p.fwd4 == 4 && p.wr < 0 && !p.alibi && !(p.softcap_pre > 0.f)));
     static std::atomic<unsigned long long> attr_done{0};
     once_per_device(attr_done, p.device, [&] {
         (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);
         (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);
+        (void)hipFuncSetAttribute((const void*)fmha_fwdpp_kernel<BF, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdppSmem);
     });
-    note_launch(m16 ? "fmha_fwdpp16_kernel" : "fmha_fwdpp_kernel", pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
+    note_launch(m16 ? "fmha_fwdpp16_kernel" : p.block_table ? "fmha_fwdpp_paged_kernel" : "fmha_fwdpp_kernel",
+                pp.persistent, pp.xcd_queues, grid.x, grid.y, grid.z, 512);
     if (m16) hipLaunchKernelGGL((fmha_fwdpp_kernel<BF, true>), grid, dim3(512), kFwdppSmem, st, pp);
+    else if (p.block_table) hipLaunchKernelGGL((fmha_fwdpp_kernel<BF, false, true>), grid, dim3(512), kFwdppSmem, st, pp);
     else hipLaunchKernelGGL((fmha_fwdpp_kernel<BF, false>), grid, dim3(512), kFwdppSmem, st, pp);
     return hipGetLastError();
 }

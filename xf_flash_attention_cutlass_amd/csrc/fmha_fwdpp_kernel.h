@@ -67,7 +67,7 @@ __device__ __forceinline__ constexpr int ppx16(int x) { return (0x78 >> (2 * x))
 
 // One (batch x kv head, 256-row query block) item.  M16: the body on the 16x16x32 MFMA shape
 // (a lane holds rows l16 and 16 + l16 of its wave's 32; per-lane operands below).
-template <bool BF16, bool M16>
+template <bool BF16, bool M16, bool PG>
 __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const int bh, const int m_block XFA_PP_ACC_PARAM) {
     constexpr int HD = 128;
     int tid = threadIdx.x;
@@ -172,9 +172,10 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     // the kv_off image (lane l lands at +16 l); K and V share the offsets (k_row == v_row)
     // (M16: the chunk XOR by row bits 2-3 goes through ppx16, so the 16x16x32 body's K row and
     // V^T reads are conflict-free too; see ppx16)
+    // (paged: the descriptor base points at the wave's 8 rows, so the row offset is lr / 4)
     const int r = 8 * wave + lr / 4;
     const int cch = 4 * hh + ((lane & 3) ^ (M16 ? ppx16((r >> 2) & 3) : ((r >> 2) & 3)));
-    const int dma0 = r * k_row * 2 + cch * 16;
+    const int dma0 = (PG ? lr / 4 : r) * k_row * 2 + cch * 16;
     // LDS read bases (kv_off image, slot 0; the ring slots are immediate offsets)
     const int sbase = (int)(size_t)smem;
     int kb[2], vb[2];
@@ -244,6 +245,38 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     const int hi_k = ok ? lim_r(pos) : 0, lo_k = ok ? lim_l(pos) : 0;
     const int near = min(max(pos + diag, lo_k), max(hi_k - 1, lo_k));
     const float alm = hi_k > lo_k ? -alw * (float)abs(pos + diag - near) : 0.f;
+    if constexpr (PG) {
+#ifndef XFA_FWDPP_STAMPS
+        // paged K/V (gen_fwdpp.py PAGED): per tile, each wave's 8 rows sit in one page (page size
+        // a power of two >= 8, fwd4_eligible); the body loads the page id from this sequence's
+        // block-table row and builds the wave's descriptors from the pools' bases (kblo.. here:
+        // pool + this kv head's offset), the page stride and the row bytes
+        const int* btab = p.block_table + (int64_t)bidx * p.bt_stride;
+        const char* kpool = reinterpret_cast<const char*>(p.k) + (int64_t)hk_i * p.k_head * 2;
+        const char* vpool = reinterpret_cast<const char*>(p.v) + (int64_t)hk_i * p.v_head * 2;
+        const int pkl = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)kpool);
+        const int pkh = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)kpool >> 32) & 0xFFFF);
+        const int pvl = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)vpool);
+        const int pvh = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)vpool >> 32) & 0xFFFF);
+        const int pstr = __builtin_amdgcn_readfirstlane((int)(p.k_batch * 2));
+        const int rowb = __builtin_amdgcn_readfirstlane(k_row * 2);
+        const int lgp = __builtin_amdgcn_readfirstlane(31 - __builtin_clz(p.page_size));
+        const int pmask = __builtin_amdgcn_readfirstlane(p.page_size - 1);
+        const int skv = __builtin_amdgcn_readfirstlane(sk);
+        const int skey0 = __builtin_amdgcn_readfirstlane(kBlockN * T0 + 8 * wave);
+        if constexpr (BF16)
+            fwdpp_pg_item_bf16(pkl, pkh, pvl, pvh, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                               p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff,
+                               loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, btab, pstr, rowb, lgp, pmask,
+                               skv, skey0);
+        else
+            fwdpp_pg_item_f16(pkl, pkh, pvl, pvh, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
+                              p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff,
+                              loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, btab, pstr, rowb, lgp, pmask,
+                              skv, skey0);
+#endif
+        return;
+    }
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
@@ -256,7 +289,7 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
 // (n-1-i, i) row-block pairs (dense) or per-XCD dynamic queues (varlen).
-template <bool BF16, bool M16 = false>
+template <bool BF16, bool M16 = false, bool PG = false>
 __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_claim[2];
@@ -301,7 +334,7 @@ __global__ void __launch_bounds__(512, 1) fmha_fwdpp_kernel(const FwdParams p) {
             bh = blockIdx.x;
             m_block = gridDim.y - 1 - blockIdx.y;
         }
-        fwdpp_item<BF16, M16>(p, smem, bh, m_block XFA_PP_ACC_ARG);
+        fwdpp_item<BF16, M16, PG>(p, smem, bh, m_block XFA_PP_ACC_ARG);
     }
 #ifdef XFA_FWDPP_STAMPS
     if ((threadIdx.x & 63) < 8) atomicAdd(&g_fwdpp_stamps[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)], acc);
