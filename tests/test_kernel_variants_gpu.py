@@ -553,3 +553,73 @@ def test_fwdpp_paged_prefill(b, h, hk, sq, lens, page, causal, window, alibi):
             finally:
                 L.fmha_set_option(b"fwd_w4", old)
             assert torch.equal(od.cpu(), out[i:i + 1]), f"seq {i}: paged != dense"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fwdpp_paged_sweep(seed):
+    """Seeded sweep of paged-K/V prefill shapes (page 8..512, GQA 1..8, ragged lengths, causal /
+    non-causal / sliding windows, ALiBi, fp16): the paged ping-pong kernel bit for bit equal to
+    the dense ping-pong kernel over the gathered cache, pages past each sequence NaN-filled"""
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    if L.fmha_get_option(b"fwd_w4") not in (2, 4):
+        pytest.skip("the ping-pong kernel is not selected under these options")
+    r = torch.Generator().manual_seed(1000 + seed)
+    ri = lambda lo, hi: int(torch.randint(lo, hi + 1, (1,), generator=r))  # noqa: E731
+    page = 2 ** ri(3, 9)
+    hk = [1, 2, 4][ri(0, 2)]
+    h = hk * [1, 2, 4, 8][ri(0, 3)]
+    b = ri(1, 3)
+    lens = [ri(1, 1500) for _ in range(b)]
+    sq = ri(1, min(lens))
+    sq = max(sq, 40 // (h // hk) + 1)          # keep sq * H/Hk > 32 (the prefill path, not decode)
+    lens = [max(n, sq) for n in lens]
+    mode = ri(0, 2)
+    causal = mode == 0
+    window = (-1, -1) if mode < 2 else (ri(0, 400), ri(0, 64))
+    alibi = ri(0, 1) == 1
+    dt = torch.float16 if ri(0, 1) else torch.bfloat16
+    nbp = (max(lens) + page - 1) // page
+    q = (torch.randn(b, sq, h, 128, generator=r) * 2).to(dt)
+    kf = torch.randn(b, nbp * page, hk, 128, generator=r).to(dt)
+    vf = torch.randn(b, nbp * page, hk, 128, generator=r).to(dt)
+    table = torch.randperm(b * nbp, generator=r).view(b, nbp).int()
+    kc = torch.full((b * nbp, page, hk, 128), float("nan")).to(dt)
+    vc = torch.full((b * nbp, page, hk, 128), float("nan")).to(dt)
+    for i, n in enumerate(lens):
+        for pi in range((n + page - 1) // page):
+            rows = min(page, n - pi * page)
+            kc[table[i, pi], :rows] = kf[i, pi * page:pi * page + rows]
+            vc[table[i, pi], :rows] = vf[i, pi * page:pi * page + rows]
+    slopes = (torch.rand(b, h, generator=r) * 0.3).to(DEV) if alibi else None
+    wl, wr = (-1, 0) if causal else window
+    qd, kcd, vcd = q.to(DEV), kc.to(DEV), vc.to(DEV)
+    o = torch.empty_like(qd)
+    tab, seqlens = table.to(DEV), torch.tensor(lens, dtype=torch.int32).to(DEV)
+    L.fmha_page_kvcache_fwd_ex(qd.data_ptr(), kcd.data_ptr(), vcd.data_ptr(), o.data_ptr(), None,
+                               tab.data_ptr(), nbp, seqlens.data_ptr(), sq, nbp * page, b, h, hk, 128,
+                               page, 128 ** -0.5, wl, wr, 0.0, slopes.data_ptr() if alibi else None, h, 1,
+                               0, 1.0, 1.0, None, dt == torch.float16, capi.stream_handle())
+    capi.check()
+    torch.cuda.synchronize()
+    kern = L.fmha_last_kernel().decode()
+    assert kern.startswith("fmha_fwdpp_paged_kernel "), kern
+    assert not torch.isnan(o).any()
+    old = L.fmha_get_option(b"fwd_w4")
+    assert L.fmha_set_option(b"fwd_w4", 2) == 0
+    try:
+        for i, n in enumerate(lens):
+            kd, vd = kf[i:i + 1, :n].to(DEV).contiguous(), vf[i:i + 1, :n].to(DEV).contiguous()
+            qi = qd[i:i + 1].contiguous()
+            od = torch.empty_like(qi)
+            sl = slopes[i:i + 1].contiguous() if alibi else None
+            L.fmha_fwd(qi.data_ptr(), kd.data_ptr(), vd.data_ptr(), od.data_ptr(), sl.data_ptr() if alibi else None,
+                       sq, n, 1, h, hk, 128, 0.0, capi.stream_handle(), None, 128 ** -0.5, None, None, wl, wr,
+                       0.0, False, dt == torch.float16, 1)
+            capi.check()
+            torch.cuda.synchronize()
+            assert L.fmha_last_kernel().decode().startswith("fmha_fwdpp_kernel "), L.fmha_last_kernel()
+            assert torch.equal(od, o[i:i + 1]), (f"seq {i}: page {page} h {h}/{hk} sq {sq} lens {lens} "
+                                                 f"causal {causal} window {window} alibi {alibi}")
+    finally:
+        L.fmha_set_option(b"fwd_w4", old)
