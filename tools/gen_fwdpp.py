@@ -29,6 +29,9 @@ m = the masked max of tile 0; a V phase whose partial row sums pass 2^slack take
 
 FEATURES (round 6): softcap and ALiBi in an out-of-line pass over the tile's raw scores before
 its softmax (feature_block; tile 0 before its max, the ALiBi max lifted by the row's best bias).
+Causal ALiBi (feat bit 2) is the linear bias w key: w off per score, the tile base folded into NM
+as a frame shift (SHIFT), the true -m kept in NMTRUE for the rare path, the row constant put
+back into the LSE by the epilogue.
 LEFTWIN: the key test is two-sided per lane, (off - LIML) <u wid; tiles before %[lw] take the
 masked step; a row with no visible key in tile 0 starts from m = +inf, so its first visible key
 sends the tile down the rare path, which takes the true max.  A step whose tile
@@ -94,6 +97,7 @@ LEFTWIN = True         # two-sided key window in the masked steps (left windows:
 LIML, TW = 96, 97      # the lane's left key limit (stepped -64 per tile); a compare temp
 PAGED = False          # emitting the paged-K/V body (fwdpp_pg_item_*): per-wave page descriptors
 SKEY, SPG, ST2 = 91, 94, 95   # (paged) this wave's next key row to set up, its page id, a temp
+SHIFT, NMTRUE = 98, 99  # (causal ALiBi, feat bit 2) this tile's frame shift c w key0, the true -m
 
 
 def addc_ret(reg, ret, pc, back):
@@ -334,17 +338,40 @@ def redo_block(dt, uid):
     tile's true (masked) max, m_new = max(m, c max); O and l scaled by 2^(m - m_new); the
     softmax redone against m_new (its row sum replaces LT).  Returns through SRA."""
     mx, t2, alpha = f"v{MISC}", f"v{MISC + 1}", f"v{MISC + 2}"
-    out = [f".Lredo_{uid}:"] + XDL_NOPS + row_max(mx)
-    out += [f"v_mul_f32 {t2}, %[c], {mx}",
-            f"v_max_f32_e64 {t2}, {t2}, -v{NM}",          # m_new = max(m_ref, c max)
-            # (LEFTWIN: a row still at NM = +inf with no visible key here keeps m_new finite,
-            # -FLT_MAX, so alpha = 2^(m - m_new) = 0, not NaN; its O and l are 0)
-            *([f"v_max_f32 {t2}, 0xff7fffff, {t2}"] if LEFTWIN else []),
-            f"v_add_f32 {alpha}, v{NM}, {t2}",             # m_new - m_ref >= 0
-            f"v_exp_f32_e64 {alpha}, -{alpha}",
-            f"v_mul_f32 v{NM}, -1.0, {t2}",
-            "s_nop 0",
-            f"v_mul_f32 v{LRUN}, v{LRUN}, {alpha}"]
+    out = [f".Lredo_{uid}:"] + XDL_NOPS
+    if FEATURES:
+        # in the true frame: this half's max lifted by its frame shift before the two lane
+        # halves' maxima meet (causal linear ALiBi: the halves' keys differ by 4, SHIFT too;
+        # SHIFT = 0 and NMTRUE = NM otherwise, bit for bit the plain path)
+        ninf = f"v{MISC + 3}"
+        out += [f"v_mov_b32 {ninf}, 0xff800000", f"v_mov_b32 {mx}, {ninf}"]
+        for v in range(32):
+            off, _ = value_info(v)
+            out += vis_test(off) + [f"v_cndmask_b32 {t2}, {ninf}, v{SBASE + v}, vcc",
+                                    f"v_max_f32 {mx}, {mx}, {t2}"]
+        out += [f"v_fma_f32 {mx}, {mx}, %[c], v{SHIFT}",
+                f"v_mov_b32 {t2}, {mx}", "s_nop 1", f"v_permlane32_swap_b32 {mx}, {t2}",
+                "s_nop 1", f"v_max_f32 {t2}, {mx}, {t2}",
+                f"v_max_f32_e64 {t2}, {t2}, -v{NMTRUE}",
+                *([f"v_max_f32 {t2}, 0xff7fffff, {t2}"] if LEFTWIN else []),
+                f"v_add_f32 {alpha}, v{NMTRUE}, {t2}",
+                f"v_exp_f32_e64 {alpha}, -{alpha}",
+                f"v_mul_f32 v{NMTRUE}, -1.0, {t2}",
+                f"v_add_f32 v{NM}, v{NMTRUE}, v{SHIFT}",
+                "s_nop 0",
+                f"v_mul_f32 v{LRUN}, v{LRUN}, {alpha}"]
+    else:
+        out += row_max(mx)
+        out += [f"v_mul_f32 {t2}, %[c], {mx}",
+                f"v_max_f32_e64 {t2}, {t2}, -v{NM}",          # m_new = max(m_ref, c max)
+                # (LEFTWIN: a row still at NM = +inf with no visible key here keeps m_new finite,
+                # -FLT_MAX, so alpha = 2^(m - m_new) = 0, not NaN; its O and l are 0)
+                *([f"v_max_f32 {t2}, 0xff7fffff, {t2}"] if LEFTWIN else []),
+                f"v_add_f32 {alpha}, v{NM}, {t2}",             # m_new - m_ref >= 0
+                f"v_exp_f32_e64 {alpha}, -{alpha}",
+                f"v_mul_f32 v{NM}, -1.0, {t2}",
+                "s_nop 0",
+                f"v_mul_f32 v{LRUN}, v{LRUN}, {alpha}"]
     for i in range(64):
         t = f"v{TMP + i % 8}"
         out += [f"v_accvgpr_read_b32 {t}, a{ABASE_O + i}", f"v_mul_f32 {t}, {t}, {alpha}",
@@ -408,22 +435,44 @@ def _alibi_ops():
     return out + sum((txt for _, _, txt in sorted(ops, key=lambda x: (x[0], x[1]))), [])
 
 
+def _alibi_linear_ops():
+    """causal ALiBi (every visible key <= pos + diag) as the reference kernel's linear bias
+    +w key (mask_hip.h:163-164): S += w off per score (one v_fmac with the offset as a literal)
+    and the tile's per-lane part w key0 folded into the exp argument: NM = NMTRUE + SHIFT with
+    SHIFT = c w key0 = fma(%[alw2], 64 (j + 1), %[akb]) — the true -m stays in NMTRUE, so the
+    shift never accumulates rounding"""
+    import struct
+    t = f"v{TMP + 7}"
+    out = [f"s_add_i32 s{ST}, s{SJ}, 1", f"s_lshl_b32 s{ST}, s{ST}, 6", f"v_cvt_f32_i32 {t}, s{ST}",
+           f"v_fma_f32 v{SHIFT}, %[alw2], {t}, %[ald]", f"v_add_f32 v{NM}, v{NMTRUE}, v{SHIFT}"]
+    for v in range(32):
+        off, _ = value_info(v)
+        lit = "0x%08x" % struct.unpack("<I", struct.pack("<f", float(off)))[0]
+        out.append(f"v_fmac_f32 v{SBASE + v}, {lit}, %[alw]")
+    return out
+
+
 def feature_block(uid):
     """the score features of the 8-wave kernel's transform (fmha_fwd_kernel.h transform_part),
     in place on this lane's 32 raw scores of tile j + 1 (SJ = j):
       bit 0 softcap: S = tanh(S pre) = 1 - 2 / (2^(2 log2e pre S) + 1)   (%[scp2] = 2 log2e pre)
       bit 1 ALiBi:   S -= w |pos + diag - key|   (%[alw] = slope / scale_softmax of the lane's
                      row, %[ald] = pos + diag - 4 hh; key = 64 (j + 1) + 4 hh + off)
+    bit 2 causal ALiBi (wr = 0): _alibi_linear_ops, 1 VALU per score.
     5 VALU per score for the softcap, 2 for ALiBi, staggered over the scores.  Three entries,
     each returning via SRA: .Lfeat (both, by bit), .Lfsc (softcap by bit: tile 0 before its max)
     and .Lfal (ALiBi by bit: tile 0 after it)."""
     out = [f".Lfeat_{uid}:", "s_bitcmp1_b32 %[feat], 0", f"s_cbranch_scc0 .Lfa_{uid}"] + _softcap_ops()
-    out += [f".Lfa_{uid}:", "s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfe_{uid}"] + _alibi_ops()
+    out += [f".Lfa_{uid}:", "s_bitcmp1_b32 %[feat], 2", f"s_cbranch_scc1 .Lfl_{uid}"]
+    out += ["s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfe_{uid}"] + _alibi_ops()
     out += [f".Lfe_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    out += [f".Lfl_{uid}:"] + _alibi_linear_ops() + ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
     out += [f".Lfsc_{uid}:", "s_bitcmp1_b32 %[feat], 0", f"s_cbranch_scc0 .Lfse_{uid}"] + _softcap_ops()
     out += [f".Lfse_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
-    out += [f".Lfal_{uid}:", "s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfle_{uid}"] + _alibi_ops()
+    out += [f".Lfal_{uid}:", "s_bitcmp1_b32 %[feat], 2", f"s_cbranch_scc1 .Lfll_{uid}"]
+    out += ["s_bitcmp1_b32 %[feat], 1", f"s_cbranch_scc0 .Lfle_{uid}"] + _alibi_ops()
     out += [f".Lfle_{uid}:", "s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
+    out += [f".Lfll_{uid}:"] + _alibi_linear_ops() + ["s_nop 3", f"s_setpc_b64 s[{SRA}:{SRA + 1}]"]
     return out
 
 
@@ -495,9 +544,13 @@ def epilogue_core(dt):
     return out
 
 
-def epilogue(dt):
-    """once per wave: the rows' epilogue (marks SST)"""
-    return [f"s_mov_b32 s{SST}, 1"] + XDL_NOPS + epilogue_core(dt)
+def epilogue(dt, tag=""):
+    """once per wave: the rows' epilogue (marks SST).  Causal ALiBi in the linear frame (feat bit
+    2): NM = NMTRUE + %[adiag] first, the -m of the kernels' |.| form, whose LSE the API converts
+    to the reference's convention (fmha_lse_alibi_kernel) as for every other kernel"""
+    fix = ([f"s_bitcmp1_b32 %[feat], 2", f"s_cbranch_scc0 .Lep{tag}_%=",
+            f"v_add_f32 v{NM}, v{NMTRUE}, %[adiag]", f".Lep{tag}_%=:"] if FEATURES else [])
+    return [f"s_mov_b32 s{SST}, 1"] + fix + XDL_NOPS + epilogue_core(dt)
 
 
 N_EPI_STORES = 9       # 8 O row stores + the LSE store
@@ -527,7 +580,8 @@ def group_program(dt, grp):
         v, stub = v_phase(dt, DLEAD - 1, "m", uid, "f", feat=False)
         f0, s0 = feat_call(uid, "f0", "fsc")
         f1, s1 = feat_call(uid, "f1", "fal")
-        out += XDL_NOPS + f0 + first_max() + [f"v_fma_f32 v{NM}, -%[c], %[alm], v{NM}"] + f1
+        out += XDL_NOPS + f0 + first_max() + [f"v_fma_f32 v{NM}, -%[c], %[alm], v{NM}",
+                                               f"v_mov_b32 v{NMTRUE}, v{NM}"] + f1
         out += v + st(ST_V) + v_wait + bar
         stub += s0 + s1
     else:
@@ -568,7 +622,7 @@ def group_program(dt, grp):
         tail += m_phase(dt, ph, qk=False) + st(ST_M) + m_wait + bar + st(ST_MW)
         v, _ = v_phase(dt, vslot, "n", uid, f"l{ph}")
         # DMA first, then the rows' stores (the youngest N_EPI_STORES may stay in flight)
-        tail += v + st(ST_V) + epilogue(dt) + st(ST_EPI)
+        tail += v + st(ST_V) + epilogue(dt, f"{'AB'[grp]}{ph}") + st(ST_EPI)
         tail += ([] if grp else [f"s_waitcnt vmcnt({NPIECE * (DLEAD - 2) + N_EPI_STORES})"]) + bar
         tail += [f"s_branch .Lnx{ph}_{uid}"]
         tail.append(f".Li{ph}_{uid}:")
@@ -581,7 +635,7 @@ def group_program(dt, grp):
     if not grp:
         out += bar                                          # A's closing phase
     # rows that never reached a last step (no visible key): their O = 0, LSE = +inf
-    out += [f"s_cmp_eq_u32 s{SST}, 0", f"s_cbranch_scc0 .Ldone_{uid}"] + epilogue(dt)
+    out += [f"s_cmp_eq_u32 s{SST}, 0", f"s_cbranch_scc0 .Ldone_{uid}"] + epilogue(dt, f"{'AB'[grp]}x")
     out += [f".Ldone_{uid}:"] + ([] if "noepiwait" in ABL else ["s_waitcnt vmcnt(0)"])
     out += st(ST_TAIL) + ["s_branch .Lend_%="]
     return out + tail + redo_block(dt, uid) + (feature_block(uid) if FEATURES else [])
@@ -592,6 +646,7 @@ def item_program(dt):
     out += ["s_waitcnt lgkmcnt(0)",
            f"v_mov_b32 v{NM}, 0", f"v_mov_b32 v{LRUN}, 0", f"v_mov_b32 v{LIM}, %[lim]",
            *([f"v_mov_b32 v{LIML}, %[liml]"] if LEFTWIN else []),
+           *([f"v_mov_b32 v{SHIFT}, 0", f"v_mov_b32 v{NMTRUE}, 0"] if FEATURES else []),
            f"s_mov_b32 s{SST}, 0"]
     if not ABL & {"nopro", "nopq"}:
         out += [f"buffer_load_dwordx4 {qtup(s)}, %[qoff], %[qsrd], 0 offen offset:{32 * s}" for s in range(8)]
@@ -620,7 +675,7 @@ SIG = ("const int kblo, const int kbhi, const int vblo, const int vbhi, const in
        "const int kb0, const int kb1, const int vb0, const int vb1, const int dma0, const int dma1, "
        "const int lim, const int qoff, const int ooff, const int loff, const int feat, "
        "const float scp2, const float alw, const float ald, const float alm, const int lw, "
-       "const int liml, const int wid, const int fw")
+       "const int liml, const int wid, const int fw, const float alw2, const float adiag")
 OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(vbhi)',
        '[kvbytes] "s"(kvbytes)', '[qsrd] "s"(qsrd)', '[osrd] "s"(osrd)', '[lsrd] "s"(lsrd)',
        '[kstep] "s"(kstep)', '[kdst] "s"(kdst)', '[ntl] "s"(ntl)', '[tw] "s"(tw)', '[ew] "s"(ew)',
@@ -629,11 +684,11 @@ OPS = ['[kblo] "s"(kblo)', '[kbhi] "s"(kbhi)', '[vblo] "s"(vblo)', '[vbhi] "s"(v
        '[dma0] "v"(dma0)', '[dma1] "v"(dma1)', '[lim] "v"(lim)', '[qoff] "v"(qoff)',
        '[ooff] "v"(ooff)', '[loff] "v"(loff)', '[feat] "s"(feat)', '[scp2] "s"(scp2)',
        '[alw] "v"(alw)', '[ald] "v"(ald)', '[alm] "v"(alm)', '[lw] "s"(lw)', '[liml] "v"(liml)',
-       '[wid] "v"(wid)', '[fw] "s"(fw)']
+       '[wid] "v"(wid)', '[fw] "s"(fw)', '[alw2] "v"(alw2)', '[adiag] "v"(adiag)']
 
 
 def clobbers():
-    regs = [f'"v{i}"' for i in range(98 if LEFTWIN else 96)] + [f'"a{i}"' for i in range(128)]
+    regs = [f'"v{i}"' for i in range(100 if FEATURES else 98 if LEFTWIN else 96)] + [f'"a{i}"' for i in range(128)]
     regs += [f'"s{i}"' for i in range(SKR, SCM + 2)] + ([f'"s{i}"' for i in range(96, 100)] if STAMPS else [])
     return ", ".join(regs + ['"vcc"', '"scc"', '"memory"'])
 

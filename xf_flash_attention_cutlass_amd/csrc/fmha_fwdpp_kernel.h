@@ -236,15 +236,23 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
     }
     // score features (gen_fwdpp.feature_block): bit 0 softcap, bit 1 ALiBi (the lane's row slope
     // in raw-score units and its distance pos + diag - 4 hh to the lane's key offset 0)
-    const int feat = __builtin_amdgcn_readfirstlane((p.softcap_pre > 0.f ? 1 : 0) | (p.alibi ? 2 : 0));
+    // bit 2: causal ALiBi (wr = 0, every visible key <= pos + diag) in the linear frame +w key
+    // (gen_fwdpp._alibi_linear_ops: one v_fmac per score instead of the |.| form's two)
+    const bool lin = p.alibi && p.wr == 0;
+    const int feat = __builtin_amdgcn_readfirstlane((p.softcap_pre > 0.f ? 1 : 0) | (p.alibi ? (lin ? 4 : 2) : 0));
     const float scp2 = p.softcap_pre * (2.f * kLog2e);
     const float alw = (p.alibi && ok) ? p.alibi[bidx * p.alibi_bstride + head] * p.alibi_mul : 0.f;
-    const float ald = (float)(pos + diag - 4 * hh - kBlockN * T0);
+    // |.| form: the distance base pos + diag - 4 hh - 64 T0; linear form: c w (64 T0 + 4 hh), the
+    // tile-invariant part of the frame shift c w key0
+    const float ald = lin ? p.scale_log2 * alw * (float)(kBlockN * T0 + 4 * hh)
+                          : (float)(pos + diag - 4 * hh - kBlockN * T0);
+    const float alw2 = p.scale_log2 * alw;                       // c w
+    const float adiag = p.scale_log2 * alw * (float)(pos + diag);   // the |.| form's row offset
     // the row's best ALiBi bias: -w times the distance from pos + diag to its nearest visible key
     // (keys [lim_l, lim_r)); tile 0's reference max is lifted by it
     const int hi_k = ok ? lim_r(pos) : 0, lo_k = ok ? lim_l(pos) : 0;
     const int near = min(max(pos + diag, lo_k), max(hi_k - 1, lo_k));
-    const float alm = hi_k > lo_k ? -alw * (float)abs(pos + diag - near) : 0.f;
+    const float alm = hi_k > lo_k ? (lin ? alw * (float)near : -alw * (float)abs(pos + diag - near)) : 0.f;
     if constexpr (PG) {
 #ifndef XFA_FWDPP_STAMPS
         // paged K/V (gen_fwdpp.py PAGED): per tile, each wave's 8 rows sit in one page (page size
@@ -267,24 +275,24 @@ __device__ __forceinline__ void fwdpp_item(const FwdParams& p, char* smem, const
         if constexpr (BF16)
             fwdpp_pg_item_bf16(pkl, pkh, pvl, pvh, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                                p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff,
-                               loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, btab, pstr, rowb, lgp, pmask,
-                               skv, skey0);
+                               loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, alw2, adiag, btab, pstr, rowb,
+                               lgp, pmask, skv, skey0);
         else
             fwdpp_pg_item_f16(pkl, pkh, pvl, pvh, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                               p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff,
-                              loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, btab, pstr, rowb, lgp, pmask,
-                              skv, skey0);
+                              loff, feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, alw2, adiag, btab, pstr, rowb,
+                              lgp, pmask, skv, skey0);
 #endif
         return;
     }
     if constexpr (BF16)
         fwdpp_item_bf16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                         p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                        feat, scp2, alw, ald, alm, l_w, liml, wid, f_w XFA_PP_ACC_ARG);
+                        feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, alw2, adiag XFA_PP_ACC_ARG);
     else
         fwdpp_item_f16(kblo, kbhi, vblo, vbhi, kvbytes, qsrd, osrd, lsrd, kstep, kdst, ntl, t_w, e_w, grp,
                        p.scale_log2, thr, kb[0], kb[1], vb[0], vb[1], dma0, dma0 + 128, lim, qoff, ooff, loff,
-                       feat, scp2, alw, ald, alm, l_w, liml, wid, f_w XFA_PP_ACC_ARG);
+                       feat, scp2, alw, ald, alm, l_w, liml, wid, f_w, alw2, adiag XFA_PP_ACC_ARG);
 }
 
 // Persistent grid (one workgroup per CU) over the items, the 4-wave kernel's orders: XCD-grouped
