@@ -125,3 +125,37 @@ def test_causal_alibi_bwd_reads_converted_lse(xfa, deterministic):
     for nm, x, r, p in zip(("dq", "dk", "dv"), got, ref, pt):
         ok, err, bound = orc.parity_ok(x.cpu(), r, p, 3.0, 1e-5)
         assert ok, f"{nm}: {err:.3g} > {bound:.3g}"
+
+
+def test_causal_alibi_long_linear_frame(xfa):
+    """The ping-pong kernel runs causal ALiBi in the linear frame (bias slope * key, the tile base
+    folded into the subtracted max, gen_fwdpp.py _alibi_linear_ops): at 8192 keys and the largest
+    slope (0.5) the frame's offsets reach 4096 in score units, so O and the LSE are checked there,
+    the LSE against the fp32 log-sum-exp with 4 fp32 ulps of its magnitude added to LSE_ATOL (the
+    reference-convention LSE is itself of that size).  One varlen sequence: a single pass, as the
+    reference forces for varlen (no split-KV heuristic at two heads)."""
+    from xf_flash_attention_cutlass_amd import capi
+    g = torch.Generator().manual_seed(8192)
+    s, h, d = 8192, 2, 128
+    q = torch.randn(s, h, d, generator=g).bfloat16()
+    k = torch.randn(s, h, d, generator=g).bfloat16()
+    v = torch.randn(s, h, d, generator=g).bfloat16()
+    cu = torch.tensor([0, s], dtype=torch.int32)
+    slopes = torch.tensor([[0.5, 2.0 ** -7]])
+    out, lse, _ = xfa.flash_attn_varlen_func(q.to(DEV), k.to(DEV), v.to(DEV), cu.to(DEV), cu.to(DEV),
+                                             s, s, causal=True, alibi_slopes=slopes.to(DEV),
+                                             return_attn_probs=True)
+    kern = capi.lib().fmha_last_kernel().decode()
+    assert kern.startswith("fmha_fwdpp_kernel "), kern
+    bias_o = orc.alibi_bias(slopes, s, s, causal=True)
+    ref, _ = orc.attention_ref(q[None], k[None], v[None], attn_bias=bias_o, causal=True)
+    pt, _ = orc.attention_ref(q[None], k[None], v[None], attn_bias=bias_o, causal=True, upcast=False,
+                              reorder_ops=True)
+    ok, err, bound = orc.parity_ok(out[None].float().cpu(), ref, pt, 2.0, 1e-5)
+    assert ok, f"O: {err:.3g} > {bound:.3g}"
+    lref = orc.attention_lse_ref(q[None], k[None], attn_bias=orc.alibi_bias_kernel(slopes, s, s, causal=True),
+                                 causal=True)[0].float()
+    lse = lse.float().cpu()                          # [h, total_q]
+    tol = LSE_ATOL + 4 * torch.finfo(torch.float32).eps * lref.abs()
+    err = (lse - lref).abs()
+    assert bool((err <= tol).all()), f"max|lse - ref| = {err.max().item():.3g}, tol {tol.max().item():.3g}"
