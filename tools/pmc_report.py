@@ -29,6 +29,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -117,7 +118,7 @@ def main():
             if long_enough and "SQ_INSTS_MFMA" in c:
                 # cycles per MFMA instruction: 64 for the block-scaled fp8 one, 16 for
                 # v_mfma_f32_16x16x32 (the M16 ping-pong body, the 16-row decode tile), else 32
-                m16 = "fmha_fwdpp_kernel<true, true>" in k or "fmha_fwdpp_kernel<false, true>" in k
+                m16 = re.search(r"fmha_fwdpp_kernel<(true|false), true", k) is not None
                 per = 64 if "fp8" in k or "fwd8" in k else 16 if (m16 or "decode" in k) else 32
                 e["mfma_util_from_insts"] = round(c["SQ_INSTS_MFMA"] * per / (4 * NUM_CUS * cyc), 4)
             if c.get("SQ_INSTS_MFMA"):
