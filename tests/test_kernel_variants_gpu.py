@@ -469,6 +469,40 @@ def test_fwdpp16_noncausal_dynamic_default():
             L.fmha_set_option(opt, old)
 
 
+def test_fwdpp_sliding_window_dynamic_default():
+    """Causal D = 128 launches with a left window that cuts the rows take the per-XCD dynamic
+    queues by default (their row blocks carry equal work past the window's width, so the static
+    pairs unbalance them); plain causal launches keep the static XCD pairs.  Bit-identical to the
+    static pairs; sampled heads against the oracle."""
+    import xf_flash_attention_cutlass_amd as xfa
+    from xf_flash_attention_cutlass_amd import capi
+    L = capi.lib()
+    B, S, H, W = 4, 2048, 16, 255      # 512 row blocks: one pass (no split-KV)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    q, k, v = (torch.randn(B, S, H, 128, device=DEV, generator=g, dtype=torch.bfloat16) for _ in range(3))
+    out = xfa.flash_attn_func(q, k, v, causal=True, window_size=(W, 0))
+    kern = L.fmha_last_kernel().decode()
+    default = L.fmha_get_option(b"fwd_w4") == 4 and L.fmha_get_option(b"fwd_dyn") == 1
+    if default:
+        assert kern.startswith("fmha_fwdpp_kernel persistent=3 xcdq=1"), kern
+    for b, hh in ((0, 0), (1, 15)):
+        qs, ks, vs = (x[b:b + 1, :, hh:hh + 1].cpu() for x in (q, k, v))
+        ref, _ = orc.attention_ref(qs, ks, vs, causal=True, window_size=(W, 0))
+        pt, _ = orc.attention_ref(qs, ks, vs, causal=True, window_size=(W, 0), upcast=False, reorder_ops=True)
+        ok, err, bound = orc.parity_ok(out[b:b + 1, :, hh:hh + 1].cpu().float(), ref, pt, 2.0)
+        assert ok, f"b{b} h{hh}: {err:.3g} > {bound:.3g}"
+    old = L.fmha_get_option(b"fwd_dyn")
+    assert L.fmha_set_option(b"fwd_dyn", 0) == 0
+    try:
+        assert torch.equal(out, xfa.flash_attn_func(q, k, v, causal=True, window_size=(W, 0)))
+        assert "persistent=2" in L.fmha_last_kernel().decode()
+    finally:
+        L.fmha_set_option(b"fwd_dyn", old)
+    xfa.flash_attn_func(q, k, v, causal=True)
+    if default:
+        assert L.fmha_last_kernel().decode().startswith("fmha_fwdpp_kernel persistent=2"), "causal keeps the pairs"
+
+
 PAGED_CASES = [
     # b, h, hk, sq, cache lens, page, causal, window, alibi
     (2, 4, 4, 300, [300, 300], 16, True, (-1, -1), False),

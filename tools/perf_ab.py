@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--noncausal", action="store_true")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--wl", type=int, default=-1, help="fwd: left window (with causal: a sliding window)")
     a = ap.parse_args()
 
     import xf_flash_attention_cutlass_amd as xfa
@@ -70,12 +71,15 @@ def main():
             pa.fwd_fp8(q8, k8, v8, None, qs, ks, vs, sc, causal, -1, -1, False)
             return
         if a.mode in ("fwd", "fwdbwd"):
-            pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)
+            pa.fwd(q, k, v, out, None, 0.0, sc, causal, a.wl, -1, 0.0, False, None)
         if a.mode in ("bwd", "fwdbwd"):
             pa.bwd(do, q, k, v, out, lse, None, None, None, None, 0.0, sc, causal, -1, -1, 0.0,
                    False, None, None)
 
     fl = 4.0 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0)
+    if a.wl >= 0 and causal:                   # visible pairs of a sliding window (wl, 0)
+        w = min(a.wl, a.s - 1)
+        fl = 4.0 * a.b * a.h * a.d * (a.s * (w + 1) - w * (w + 1) / 2)
     fl *= {"fwd": 1.0, "bwd": 2.5, "fwdbwd": 3.5, "fwd_fp8": 1.0}[a.mode]
     res = {str(vv): [] for vv in variants}
     kern = {}

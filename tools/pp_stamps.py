@@ -23,6 +23,7 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--noncausal", action="store_true")
     ap.add_argument("--w4", type=int, default=2, help="fwd_w4: 2 the 32x32x16 body, 3 the 16x16x32 body")
+    ap.add_argument("--wl", type=int, default=-1, help="left window (causal: a sliding window)")
     ap.add_argument("--iters", type=int, default=3,
                     help="launches summed (the device counters are 32-bit: keep 256 CUs x launches x cycles < 2^32)")
     a = ap.parse_args()
@@ -41,7 +42,7 @@ def main():
 
     def run():
         lib.fmha_fwd(P(q), P(k), P(v), P(o), None, s, s, b, h, h, d, 0.0, stream, None, d ** -0.5,
-                     None, P(lse), -1, wr, 0.0, False, False, 0)
+                     None, P(lse), a.wl, wr, 0.0, False, False, 0)
     buf = (ctypes.c_uint * 64)()
     for _ in range(5):
         run()
@@ -49,7 +50,7 @@ def main():
     for _ in range(a.iters):
         run()
     assert st(buf, 1) == 0
-    print(f"C2 {'non-causal' if a.noncausal else 'causal'}, {a.iters} launches, kernel {lib.fmha_last_kernel().decode()}")
+    print(f"C2 {'non-causal' if a.noncausal else 'causal'} window left {a.wl}, {a.iters} launches, kernel {lib.fmha_last_kernel().decode()}")
     print("wave | " + " | ".join(CLASSES) + " | total Mcyc")
     for w in range(8):
         vals = [buf[w * 8 + c] for c in range(len(CLASSES))]

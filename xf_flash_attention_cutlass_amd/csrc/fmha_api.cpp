@@ -363,11 +363,14 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     // dynamic item queue: ragged (varlen) row blocks balance across CUs as they finish; also the
     // dense D = 128 launches without a right window (the 16x16x32 ping-pong body), whose equal
     // items ran 0.7-1.0 % faster from the per-XCD queues than from the static XCD pairs on two
-    // leases (causal launches keep the pairs, which balance their item sizes)
+    // leases (causal launches keep the pairs, which balance their item sizes),
+    // and the D = 128 launches with a left window, whose row blocks past the window's width all
+    // carry the same work, so the pairs unbalance them (+6 % at (1023, 0), +2 % at (255, 0))
     p.work_ctr = nullptr;
     const int dyn = o.fwd_dyn.load();
     const bool nc16 = p.d == 128 && p.wr < 0 && p.fwd4 == 4 && !p.alibi && !(p.softcap_pre > 0.f);
-    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && (p.cu_seqlens_q || nc16)))) {
+    const bool win = p.d == 128 && p.fwd4 == 4 && p.wl >= 0 && p.wl < p.seqlen_k;  // causal: wl = seqlen_k
+    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && (p.cu_seqlens_q || nc16 || win)))) {
         p.work_ctr = counter_get(st);
         if (!p.work_ctr) { fail(3, "could not allocate the item-queue counters"); return; }
     }
