@@ -306,6 +306,7 @@ FEAT_CASES = [
     # b, h, hk, sq, sk, causal, window, alibi, softcap
     (2, 4, 4, 700, 700, True, (-1, -1), True, 0.0),
     (1, 8, 2, 513, 1025, False, (-1, -1), True, 0.0),
+    (1, 8, 2, 513, 1025, True, (-1, -1), True, 0.0),      # causal ALiBi, sq < sk: linear frame, diag > 0
     (2, 4, 4, 300, 900, True, (-1, -1), False, 30.0),
     (1, 4, 2, 1024, 1024, False, (-1, 200), True, 20.0),
     (2, 8, 8, 257, 129, True, (-1, -1), True, 15.0),     # sq > sk: rows with no key
