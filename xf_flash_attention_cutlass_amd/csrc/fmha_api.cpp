@@ -365,7 +365,8 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     // items ran 0.7-1.0 % faster from the per-XCD queues than from the static XCD pairs on two
     // leases (causal launches keep the pairs, which balance their item sizes),
     // and the D = 128 launches with a left window, whose row blocks past the window's width all
-    // carry the same work, so the pairs unbalance them (+6 % at (1023, 0), +2 % at (255, 0))
+    // carry the same work, so the pairs unbalance them (+7 % at (1023, 0), +4 % at (255, 0);
+    // profiles/r06_window_dyn_ab.log)
     p.work_ctr = nullptr;
     const int dyn = o.fwd_dyn.load();
     const bool nc16 = p.d == 128 && p.wr < 0 && p.fwd4 == 4 && !p.alibi && !(p.softcap_pre > 0.f);
