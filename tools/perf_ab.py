@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--noncausal", action="store_true")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--alibi", action="store_true", help="fwd: ALiBi slopes 2^-(8 (h+1) / H)")
+    ap.add_argument("--softcap", type=float, default=0.0)
     ap.add_argument("--wl", type=int, default=-1, help="fwd: left window (with causal: a sliding window)")
     a = ap.parse_args()
 
@@ -59,6 +61,8 @@ def main():
     pa = xfa.paged_attn
     sc = a.d ** -0.5
     lse = pa.fwd(q, k, v, out, None, 0.0, sc, causal, -1, -1, 0.0, False, None)[5]
+    slopes = (2.0 ** (-8.0 * torch.arange(1, a.h + 1, device="cuda") / a.h)).float().expand(a.b, a.h).contiguous() \
+        if a.alibi else None
 
     if a.mode == "fwd_fp8":
         def e4m3(t):                           # per-tensor scale to the e4m3 range (as bench.py)
@@ -71,7 +75,7 @@ def main():
             pa.fwd_fp8(q8, k8, v8, None, qs, ks, vs, sc, causal, -1, -1, False)
             return
         if a.mode in ("fwd", "fwdbwd"):
-            pa.fwd(q, k, v, out, None, 0.0, sc, causal, a.wl, -1, 0.0, False, None)
+            pa.fwd(q, k, v, out, slopes, 0.0, sc, causal, a.wl, -1, a.softcap, False, None)
         if a.mode in ("bwd", "fwdbwd"):
             pa.bwd(do, q, k, v, out, lse, None, None, None, None, 0.0, sc, causal, -1, -1, 0.0,
                    False, None, None)

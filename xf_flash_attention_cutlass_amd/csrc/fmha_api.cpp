@@ -366,12 +366,15 @@ void run_fwd(FwdParams& p, bool bf16, hipStream_t st, int num_splits_req) {
     // leases (causal launches keep the pairs, which balance their item sizes),
     // and the D = 128 launches with a left window, whose row blocks past the window's width all
     // carry the same work, so the pairs unbalance them (+7 % at (1023, 0), +4 % at (255, 0);
-    // profiles/r06_window_dyn_ab.log)
+    // profiles/r06_window_dyn_ab.log), and the non-causal ALiBi launches (32x32x16 body, +0.5 to
+    // +3.2 % on two boxes; non-causal softcap measured -0.4 % and keeps the pairs:
+    // r06_noncausal_feat_ab.log)
     p.work_ctr = nullptr;
     const int dyn = o.fwd_dyn.load();
     const bool nc16 = p.d == 128 && p.wr < 0 && p.fwd4 == 4 && !p.alibi && !(p.softcap_pre > 0.f);
+    const bool ncab = p.d == 128 && p.wr < 0 && p.fwd4 == 4 && p.alibi;
     const bool win = p.d == 128 && p.fwd4 == 4 && p.wl >= 0 && p.wl < p.seqlen_k;  // causal: wl = seqlen_k
-    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && (p.cu_seqlens_q || nc16 || win)))) {
+    if (!p.decode && splits == 1 && (dyn == 2 || (dyn == 1 && (p.cu_seqlens_q || nc16 || ncab || win)))) {
         p.work_ctr = counter_get(st);
         if (!p.work_ctr) { fail(3, "could not allocate the item-queue counters"); return; }
     }
