@@ -83,6 +83,7 @@ VPH_NOPS = ["s_nop 7", "s_nop 7"]              # (a V phase: after its first DMA
 NPIECE = 4             # LDS-DMA pieces per wave per tile (A's publish wait keeps them in flight)
 EPI_SCALE = None       # an SGPR operand O is also scaled by in the epilogue (fp8: %[vsc])
 DMAMIX = True          # the V phase's DMA pieces 2-4 spread through the softmax (else all first)
+PRO_V0 = False         # (experiment) the prologue's wait leaves tile 0's V pieces in flight
 STAMPS = False         # diagnostic build: s_memtime per phase boundary, summed per class in lanes
                        # 0-7 of %[acc] (fmha_fwdpp_kernel.h XFA_FWDPP_STAMPS; read its SHARES only)
 RING = 4               # K / V tile slots in LDS
@@ -663,6 +664,9 @@ def item_program(dt):
         out += (pg_load() if PAGED else []) + dma_advance()
     # Q and tile 0 landed, published
     w = NPIECE * (DLEAD - 2) if not ABL & {"nopro", "nopkv"} else 0
+    if PRO_V0 and w:
+        w += 2      # tile 0's two V pieces (issued after its K pieces) stay in flight: PV(0)
+                    # comes after both groups' next vmcnt waits
     out += ([] if "nopro" in ABL else [f"s_waitcnt vmcnt({w})"]) + ["s_barrier"]
     out += ["s_cmp_eq_u32 %[grp], 0", "s_cbranch_scc0 .LgrpB_%="]
     out += group_program(dt, 0) + [".LgrpB_%=:"] + group_program(dt, 1) + [".Lend_%=:"]
@@ -740,7 +744,9 @@ if __name__ == "__main__":
     ap.add_argument("--abl", default="", help="timing ablations, comma list (results invalid)")
     ap.add_argument("--stamps", action="store_true", help="diagnostic phase stamps (XFA_FWDPP_STAMPS)")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--pro-v0", action="store_true", help="prologue waits for Q and K0 only")
     a = ap.parse_args()
+    PRO_V0 = a.pro_v0
     ABL = set(x for x in a.abl.split(",") if x)
     STAMPS = a.stamps
     emit(a.out)
